@@ -1,0 +1,313 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident batched RC4 throughput on MI355X.
+
+Metric (BASELINE.json): "RC4 GiB/s device-resident (batched session payloads)
+at 1/2/4/8 MI355X".  One step = one zrc4_crypt pass (batched
+RC4Encryption::encryption, depends/rc4/rc4_encryption.h:74-93) over one batch
+of the chosen workload:
+
+  cfg2 (default, BASELINE configs[1]): 4 096 sessions x 1 KiB per GPU
+  cfg3: 65 536 x 256 B   cfg4: 1 024 x 64 KiB   cfg5: 524 288 x 1 KiB
+
+Multi-GPU: one process per GPU (torchrun), sessions shard across ranks with no
+collective on the data path; each rank runs the same per-GPU
+batch over its own global session ids -> "scaling": "weak".  torch.distributed
+is used only for the start/stop barrier and the max-over-ranks time.
+
+HBM honesty: each rank rotates over R distinct batches (distinct sessions,
+states and payload buffers) totalling >= --footprint-mib (default 640 MiB, i.e.
+beyond the 256 MiB Infinity Cache), so successive steps do not re-hit caches.
+
+Inputs are synthetic (zsummerx_amd/synth.py): mt19937_64 keys
+and payload, states pre-advanced (sid*37)%1000 bytes; KSA and pre-advance run
+before the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "RC4 GiB/s device-resident (batched session payloads) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+STATE_BYTES = 516              # 258-B state load + store per session
+GIB = float(1 << 30)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return ws, rank, local
+
+
+def algorithmic_bytes(S: int, L: int) -> int:
+    """B = 2*sum(L) + 516*S  (payload read+write + state load+store)."""
+    return 2 * S * L + STATE_BYTES * S
+
+
+def rotation_batches(S: int, L: int, footprint_mib: int) -> int:
+    per_batch = S * L + S * 256
+    return max(1, math.ceil(footprint_mib * (1 << 20) / per_batch))
+
+
+def shard_first(rank: int, R: int, S: int) -> int:
+    """Global id of rank r's first session: ranks own disjoint session ranges."""
+    return rank * R * S
+
+
+# ------------------------------------------------------------------ GPU leg
+class GpuRunner:
+    """Owns the device buffers of R rotating batches on one GPU."""
+
+    def __init__(self, torch, device: int, S: int, L: int, R: int, first: int):
+        from zsummerx_amd import Context, synth
+        self.torch, self.S, self.L, self.R = torch, S, L, R
+        dev = torch.device("cuda", device)
+        self.ctx = Context(device, S * R)
+        self.stream = torch.cuda.current_stream(dev)
+        t0 = time.time()
+        keys = synth.keys(first, S * R).reshape(-1)
+        adv = synth.advance(first, S * R)
+        payload = synth.payload(first * L, S * R * L, threads=8)
+        log(f"[rank gen] {S*R} sessions, {payload.nbytes/2**20:.0f} MiB payload in {time.time()-t0:.1f}s")
+        T = lambda a: torch.from_numpy(a).to(dev)
+        n = S * R
+        key_len = T(np.full(n, 16, dtype=np.int32))
+        key_off = T(np.arange(n, dtype=np.int64) * 16)
+        self.ctx.ksa(key_len, key_off, T(keys), stream=self.stream)
+        scratch = torch.zeros(1000, dtype=torch.uint8, device=dev)
+        self.ctx.crypt(scratch, torch.zeros(n, dtype=torch.int64, device=dev),
+                       T(adv.view(np.int32)), stream=self.stream)
+        self.payload = T(payload)
+        self.off = T((np.arange(n, dtype=np.int64) * L))
+        self.len = T(np.full(n, L, dtype=np.int32))
+        self.ids = T(np.arange(n, dtype=np.int32))
+        self.ctx.sync(self.stream)
+        # cached raw arguments per batch: zrc4_crypt(ctx, ids, payload, off, len, n, stream)
+        lib, h, st = self.ctx._lib, self.ctx._h, C.c_void_p(self.stream.cuda_stream)
+        self._fn = lib.zrc4_crypt
+        self._args = []
+        for b in range(R):
+            self._args.append((h, C.c_void_p(self.ids.data_ptr() + 4 * b * S), C.c_void_p(self.payload.data_ptr()),
+                               C.c_void_p(self.off.data_ptr() + 8 * b * S), C.c_void_p(self.len.data_ptr() + 4 * b * S),
+                               S, st))
+
+    def step(self, i: int) -> None:
+        rc = self._fn(*self._args[i % self.R])
+        if rc:
+            raise RuntimeError(f"zrc4_crypt failed: {rc}")
+
+    def sync(self) -> None:
+        self.torch.cuda.synchronize()
+
+    def check(self) -> None:
+        self.ctx.sync(self.stream)
+
+
+def run_gpu(args, ws, rank, local):
+    import torch
+    import torch.distributed as dist
+
+    if ws > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    S, L = CONFIG_SHAPES[args.workload]
+    R = rotation_batches(S, L, args.footprint_mib) if args.footprint_mib > 0 else 1
+    runner = GpuRunner(torch, local, S, L, R, shard_first(rank, R, S))
+
+    def barrier():
+        if ws > 1:
+            dist.barrier()
+
+    for i in range(args.warmup):
+        runner.step(i)
+    runner.sync()
+
+    # kernel-duration probe: HIP events bracketing each launch on the launch stream
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    barrier()
+    runner.sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(runner.stream)
+        runner.step(args.warmup + i)
+        ev[i][1].record(runner.stream)
+    runner.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    runner.check()
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if ws > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    tmax = float(t.item())
+    k = torch.tensor([statistics.mean(kern_ms)], dtype=torch.float64, device="cuda")
+    if ws > 1:
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+    kern_avg_ms = float(k.item())
+
+    res = None
+    if rank == 0:
+        total_payload = ws * args.steps * S * L
+        res = build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload)
+        if args.cpu_seconds > 0 and ws == 1:
+            res["cpu_baseline"] = cpu_baseline(args, S, L)
+        else:
+            res["cpu_baseline"] = None
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return res
+
+
+CONFIG_SHAPES = {"cfg2": (4096, 1024), "cfg3": (65536, 256), "cfg4": (1024, 65536),
+                 "cfg5": (524288, 1024)}
+CONFIG_TEXT = {"cfg2": "4096 sessions x 1 KiB per GPU (BASELINE configs[1])",
+               "cfg3": "65536 sessions x 256 B per GPU (BASELINE configs[2])",
+               "cfg4": "1024 sessions x 64 KiB per GPU (BASELINE configs[3])",
+               "cfg5": "524288 sessions x 1 KiB per GPU (BASELINE configs[4] total)"}
+
+
+def latency_ceiling(S: int, L: int, cyc_per_byte: float, clock_ghz: float = 2.4,
+                    resident: int = 131072) -> float:
+    """Chain-bound payload rate (GiB/s): min(S, resident) chains x clock / cycles-per-byte."""
+    return min(S, resident) * clock_ghz * 1e9 / cyc_per_byte / GIB
+
+
+def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
+    value = total_payload / tmax / GIB
+    B = algorithmic_bytes(S, L)
+    achieved = B / (kern_avg_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.workload)
+    return {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(tmax / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (mt19937_64 keys seed 1, payload seed 42, pre-advance (sid*37)%1000)",
+        "config": {"workload": f"{args.workload}: {CONFIG_TEXT[args.workload]}",
+                   "sessions_per_gpu": S, "payload_bytes_per_session": L,
+                   "global_sessions_per_step": S * ws, "rotation_batches_per_gpu": R,
+                   "footprint_mib_per_gpu": round(R * S * (L + 256) / 2**20, 1),
+                   "parallelism": f"shard{ws} (sessions split across GPUs, no collective)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": traffic,
+                     "kernel": "zrc4::crypt_kernel",
+                     "algorithmic_bytes_per_launch": B,
+                     "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
+                     "kernel_min_us": round(min(kern_ms) * 1e3, 3)},
+        "latency_ceiling_gibs": {"note": "chain-bound payload rate min(S,131072 resident)*2.4GHz/L_cyc",
+                                 "L70": round(latency_ceiling(S, L, 70), 1),
+                                 "L130": round(latency_ceiling(S, L, 130), 1)},
+    }
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    p = ROOT / "profiles" / f"pmc_{workload}.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+# ------------------------------------------------------------- CPU baseline
+def cpu_baseline(args, S, L):
+    """The oracle restatement (a -O3 C port of rc4_encryption.h:74-93) timed on
+    this host on a bounded sample of the same workload (same keys, payload and
+    pre-advance as rank 0's first batch).  Reported, not optimised against."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle  # cpu_baseline leg only
+    from zsummerx_amd import synth
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, args.cpu_threads))
+    w = synth.make(0, S, L, threads=8)
+    ob = pyoracle.Batch(S)
+    ob.make_sbox(w.keys, w.key_off, w.key_len)
+    ob.crypt(np.zeros(1000, dtype=np.uint8), np.zeros(S, dtype=np.uint64), w.adv)
+    budget = args.cpu_seconds
+
+    def timed(threads, secs):
+        pay = w.payload.copy()
+        runs = []
+        t_end = time.perf_counter() + secs
+        while len(runs) < 5 or time.perf_counter() < t_end:
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                ob.crypt(pay, w.off, w.length, threads=threads)
+                reps += 1
+                dt = time.perf_counter() - t0
+                if dt >= 0.2:
+                    break
+            runs.append(reps * S * L / dt / GIB)
+            if len(runs) >= 50:
+                break
+        return statistics.median(runs)
+
+    one = timed(1, budget / 2)
+    many = timed(cores, budget / 2) if cores > 1 else one
+    return {"value": round(many, 4), "unit": "GiB/s", "cores": cores, "kind": "port",
+            "value_1thread": round(one, 4),
+            "sample": f"{args.workload} batch ({S} x {L} B) re-crypted repeatedly, "
+                      f"~{budget:.0f}s total: median of >=5 runs of >=200 ms, 1 thread then {cores} threads"}
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--workload", choices=sorted(CONFIG_SHAPES), default="cfg2")
+    p.add_argument("--footprint-mib", type=int, default=640,
+                   help="rotate over distinct batches totalling this many MiB per GPU (0 = one batch)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="CPU baseline time budget on rank 0 at N=1 (0 disables)")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    ws, rank, local = dist_env()
+    if ws != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE")
+    res = run_gpu(args, ws, rank, local)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+/*
+ * zrc4.h -- C-ABI of the MI355X-native RC4 payload-encryption path for
+ * zsummerX (the drop-in behind SessionOptions::_rc4TcpEncryption).
+ *
+ * Reference interface this boundary replaces
+ * (/root/reference, read-only):
+ *   class RC4Encryption                      depends/rc4/rc4_encryption.h:43-99
+ *     void makeSBox(std::string obscure)     depends/rc4/rc4_encryption.h:46-72
+ *     void encryption(unsigned char*, int)   depends/rc4/rc4_encryption.h:74-93
+ *     int _x, _y, _box[256]                  depends/rc4/rc4_encryption.h:96-98
+ *   reached only from TcpSession:
+ *     seeding  _rc4StateRead/_rc4StateWrite.makeSBox   src/frame/session.cpp:110-111
+ *     decrypt  _rc4StateRead.encryption(recv tail)     src/frame/session.cpp:313-323
+ *     encrypt  _rc4StateWrite.encryption(_sending)     src/frame/session.cpp:496-499,
+ *                                                      535-538, 603-606
+ *   switch    SessionOptions::_rc4TcpEncryption (empty = off)
+ *                                                      include/zsummerX/frame/config.h:196
+ *
+ * Model.  A context owns one device (HIP/gfx950) and a device-resident arena of
+ * `capacity` RC4 streams ("slots"; a TcpSession owns two: read and write).  A
+ * slot's state is the reference state (S-box + x + y) held as 258 bytes.  The
+ * batched entry points take DEVICE pointers and are stream-ordered and
+ * asynchronous; the *_host entry points take host pointers and block.
+ *
+ * Conventions (all functions):
+ *   - return 0 (ZRC4_OK) or a negative ZRC4_ERR_* code; nothing throws across
+ *     the ABI; zrc4_strerror() names a code.
+ *   - ids == NULL means the identity map (batch entry i -> slot i).
+ *   - a slot may appear at most once per call; len == 0 is a no-op for that
+ *     slot (reference: `length <= 0` never enters the loop, :81).
+ *   - calls on one context are serialised by the caller (one event-loop
+ *     thread, as the reference: include/zsummerX/frame/manager.h:98-110);
+ *     concurrent calls on different streams must touch disjoint 256-slot
+ *     groups (slot / 256).
+ *   - no CPU fallback: with no usable gfx950 device zrc4_create fails with
+ *     ZRC4_ERR_NO_DEVICE.
+ *   - device-side faults of a batched call (a slot id >= capacity) are latched
+ *     and reported by the next zrc4_sync() as ZRC4_ERR_SLOT_RANGE; the affected
+ *     entries are skipped (caller closes those sessions, as the reference does
+ *     on BCT_CORRUPTION, src/frame/session.cpp:355-361).
+ */
+#ifndef ZRC4_H
+#define ZRC4_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZRC4_OK 0
+#define ZRC4_ERR_INVALID_ARG (-1)
+#define ZRC4_ERR_NO_DEVICE (-2)
+#define ZRC4_ERR_OUT_OF_MEMORY (-3)
+#define ZRC4_ERR_LAUNCH (-4)
+#define ZRC4_ERR_SLOT_RANGE (-5)
+#define ZRC4_ERR_HIP (-6)
+
+/* Slots are grouped 256 to a 64 KiB device image (the LDS image of one
+ * workgroup); capacity is rounded up to a multiple of this. */
+#define ZRC4_GROUP_SLOTS 256u
+#define ZRC4_STATE_BYTES 258u
+
+typedef struct zrc4_ctx zrc4_ctx;
+
+/* Create a context on HIP device `device` with room for `capacity` streams.
+ * Replaces: the per-session RC4Encryption members (session.h:115-116). */
+int zrc4_create(zrc4_ctx **out, int device, uint32_t capacity);
+int zrc4_destroy(zrc4_ctx *ctx);
+uint32_t zrc4_capacity(const zrc4_ctx *ctx);
+
+/* Batched KSA (RC4Encryption::makeSBox, rc4_encryption.h:46-72) for n slots.
+ * Entry i seeds slot ids[i] from keys[key_off[i] .. key_off[i]+key_len[i]);
+ * key bytes may be NUL; key_len 0 gives the identity S-box with x = y = 0.
+ * Device pointers; asynchronous on `stream` (hipStream_t, NULL = default). */
+int zrc4_ksa(zrc4_ctx *ctx, const uint32_t *ids, const uint8_t *keys,
+             const uint64_t *key_off, const uint32_t *key_len, uint32_t n,
+             void *stream);
+
+/* Batched PRGA+XOR (RC4Encryption::encryption, rc4_encryption.h:74-93), in
+ * place: entry i crypts payload[off[i] .. off[i]+len[i]) with slot ids[i] and
+ * advances that slot by len[i] bytes.  Device pointers; asynchronous. */
+int zrc4_crypt(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payload,
+               const uint64_t *off, const uint32_t *len, uint32_t n,
+               void *stream);
+
+/* Host-pointer variants: copy to the device (pinned staging), run, copy back,
+ * block until done.  payload_bytes bounds the host payload buffer. */
+int zrc4_ksa_host(zrc4_ctx *ctx, const uint32_t *ids, const uint8_t *keys,
+                  size_t keys_bytes, const uint64_t *key_off,
+                  const uint32_t *key_len, uint32_t n);
+int zrc4_crypt_host(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payload,
+                    size_t payload_bytes, const uint64_t *off,
+                    const uint32_t *len, uint32_t n);
+
+/* Single-stream drop-ins with the reference's exact argument meaning:
+ *   zrc4_make_sbox  == RC4Encryption::makeSBox(std::string(key, keylen))
+ *   zrc4_encryption == RC4Encryption::encryption(data, length) (host data,
+ *                      in place, length <= 0 is a no-op) */
+int zrc4_make_sbox(zrc4_ctx *ctx, uint32_t id, const uint8_t *key,
+                   size_t keylen);
+int zrc4_encryption(zrc4_ctx *ctx, uint32_t id, uint8_t *data, int length);
+
+/* Wait for `stream`, then report (and clear) any latched device-side fault. */
+int zrc4_sync(zrc4_ctx *ctx, void *stream);
+
+/* Export / import one slot's state: S-box bytes + x + y (the reference's
+ * int _box[256], _x, _y narrowed to bytes; values are always in [0,255]). */
+int zrc4_get_state(zrc4_ctx *ctx, uint32_t id, uint8_t sbox[256], uint8_t *x,
+                   uint8_t *y);
+int zrc4_set_state(zrc4_ctx *ctx, uint32_t id, const uint8_t sbox[256],
+                   uint8_t x, uint8_t y);
+
+const char *zrc4_strerror(int code);
+const char *zrc4_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZRC4_H */

@@ -1,0 +1,135 @@
+/*
+ * oracle/rc4_oracle.c -- TEST INFRASTRUCTURE ONLY (see rc4_oracle.h).
+ *
+ * A plain-C restatement of RC4Encryption from
+ * /root/reference/depends/rc4/rc4_encryption.h.  The per-byte work keeps the
+ * reference's shape (int S-box, read S[x], update y, swap, keystream read) so
+ * that, compiled -O3, it is a faithful single-core timing baseline; the
+ * release flags of the reference are -O3 (CMakeLists.txt:109-111).
+ */
+#define _POSIX_C_SOURCE 200809L
+#include "rc4_oracle.h"
+
+#include <pthread.h>
+#include <string.h>
+#include <time.h>
+
+/* KSA.  Follows rc4_encryption.h:46-72:
+ *   x = y = 0; box = identity;
+ *   if key non-empty: for i in 0..255:
+ *       j = (u8)(j + box[i] + key[k]); swap(box[i], box[j]); k = (k+1) % len
+ * Key bytes are read as unsigned char (:63); an empty key leaves the identity
+ * box (:56); only the first 256 key bytes can influence the result. */
+void oracle_make_sbox(oracle_rc4_state *st, const uint8_t *key, size_t keylen)
+{
+    st->x = 0;
+    st->y = 0;
+    for (int i = 0; i < 256; ++i)
+        st->box[i] = i;
+    if (keylen == 0)
+        return;
+    unsigned j = 0;
+    size_t k = 0;
+    for (int i = 0; i < 256; ++i) {
+        int v = st->box[i];
+        j = (j + (unsigned)v + key[k]) & 0xFFu;
+        st->box[i] = st->box[j];
+        st->box[j] = v;
+        if (++k == keylen)
+            k = 0;
+    }
+}
+
+/* PRGA + XOR, in place.  Follows rc4_encryption.h:74-93: for each byte
+ *   x = (u8)(x+1); a = box[x]; y = (u8)(y+a);
+ *   b = box[x] = box[y]; box[y] = a; data[i] ^= box[(u8)(a+b)]
+ * x and y are loaded from / stored back to the state around the loop
+ * (:78-79, :91-92).  length <= 0 leaves data and state untouched. */
+void oracle_encryption(oracle_rc4_state *st, uint8_t *data, long length)
+{
+    unsigned x = (unsigned)st->x, y = (unsigned)st->y;
+    int *box = st->box;
+    for (long i = 0; i < length; ++i) {
+        x = (x + 1) & 0xFFu;
+        int a = box[x];
+        y = (y + (unsigned)a) & 0xFFu;
+        int b = box[y];
+        box[x] = b;
+        box[y] = a;
+        data[i] ^= (uint8_t)box[(unsigned)(a + b) & 0xFFu];
+    }
+    st->x = (int)x;
+    st->y = (int)y;
+}
+
+void oracle_make_sbox_batch(oracle_rc4_state *st, const uint8_t *keys,
+                            const uint64_t *key_off, const uint32_t *key_len,
+                            uint32_t n)
+{
+    for (uint32_t i = 0; i < n; ++i)
+        oracle_make_sbox(&st[i], keys + key_off[i], key_len[i]);
+}
+
+typedef struct {
+    oracle_rc4_state *st;
+    uint8_t *payload;
+    const uint64_t *off;
+    const uint32_t *len;
+    uint32_t n;
+    int tid, nthreads;
+} crypt_job;
+
+static void *crypt_worker(void *arg)
+{
+    crypt_job *j = (crypt_job *)arg;
+    for (uint32_t i = (uint32_t)j->tid; i < j->n; i += (uint32_t)j->nthreads)
+        oracle_encryption(&j->st[i], j->payload + j->off[i], (long)j->len[i]);
+    return NULL;
+}
+
+void oracle_crypt_batch(oracle_rc4_state *st, uint8_t *payload,
+                        const uint64_t *off, const uint32_t *len, uint32_t n,
+                        int threads)
+{
+    if (threads <= 1) {
+        crypt_job j = {st, payload, off, len, n, 0, 1};
+        crypt_worker(&j);
+        return;
+    }
+    if (threads > 256)
+        threads = 256;
+    pthread_t tids[256];
+    crypt_job jobs[256];
+    for (int t = 0; t < threads; ++t) {
+        crypt_job j = {st, payload, off, len, n, t, threads};
+        jobs[t] = j;
+        pthread_create(&tids[t], NULL, crypt_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; ++t)
+        pthread_join(tids[t], NULL);
+}
+
+void oracle_state_to_bytes(const oracle_rc4_state *st, uint8_t sbox[256],
+                           uint8_t *x, uint8_t *y)
+{
+    for (int i = 0; i < 256; ++i)
+        sbox[i] = (uint8_t)st->box[i];
+    *x = (uint8_t)st->x;
+    *y = (uint8_t)st->y;
+}
+
+void oracle_state_from_bytes(oracle_rc4_state *st, const uint8_t sbox[256],
+                             uint8_t x, uint8_t y)
+{
+    for (int i = 0; i < 256; ++i)
+        st->box[i] = sbox[i];
+    st->x = x;
+    st->y = y;
+}
+
+double oracle_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}

@@ -1,0 +1,61 @@
+// oracle/ref_shim.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// Compiles the REAL reference RC4 (/root/reference/depends/rc4/rc4_encryption.h,
+// included where it lies, never copied) behind a tiny extern "C" surface so the
+// golden-fixture generator (tests/golden/make_golden.py) and the CPU-only tests
+// can run the reference itself.  Built by oracle/Makefile into
+// oracle/_ref/libzrc4_ref.so, only when /root/reference is present.
+//
+// The reference header includes nothing itself; its includers provide <string>
+// first (include/zsummerX/common/common.h:78 comes after the std headers).
+#include <string>
+#include <cstring>
+#include <cstdint>
+#include <chrono>
+#include <rc4/rc4_encryption.h>
+
+static_assert(sizeof(RC4Encryption) == 2 * sizeof(int) + 256 * sizeof(int),
+              "reference state is int _x, _y, _box[256] (rc4_encryption.h:96-98)");
+
+extern "C" {
+
+int zrc4_ref_state_size(void) { return (int)sizeof(RC4Encryption); }
+
+// RC4Encryption::makeSBox(std::string) -- rc4_encryption.h:46-72.  The key is
+// built with an explicit length so embedded NULs survive, as std::string does.
+void zrc4_ref_make_sbox(void *st, const uint8_t *key, size_t keylen)
+{
+    std::string k(reinterpret_cast<const char *>(key), keylen);
+    static_cast<RC4Encryption *>(st)->makeSBox(k);
+}
+
+// RC4Encryption::encryption(unsigned char*, int) -- rc4_encryption.h:74-93.
+void zrc4_ref_encryption(void *st, uint8_t *data, int length)
+{
+    static_cast<RC4Encryption *>(st)->encryption(data, length);
+}
+
+// Read the private state out of the standard-layout object: int _x, _y,
+// _box[256] in declaration order (rc4_encryption.h:96-98).
+void zrc4_ref_get_state(const void *st, uint8_t sbox[256], uint8_t *x, uint8_t *y)
+{
+    int raw[258];
+    std::memcpy(raw, st, sizeof(raw));
+    *x = (uint8_t)raw[0];
+    *y = (uint8_t)raw[1];
+    for (int i = 0; i < 256; ++i) sbox[i] = (uint8_t)raw[2 + i];
+}
+
+// Cross-timing helper: crypt n sessions (state array of n objects), return
+// seconds spent in encryption() calls only (KSA excluded), single thread.
+double zrc4_ref_crypt_batch(void *states, uint8_t *payload, const uint64_t *off,
+                            const uint32_t *len, uint32_t n)
+{
+    RC4Encryption *s = static_cast<RC4Encryption *>(states);
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0; i < n; ++i) s[i].encryption(payload + off[i], (int)len[i]);
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+}  // extern "C"

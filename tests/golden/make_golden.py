@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures from the REAL reference RC4.
+
+Run in the survey/build container, where /root/reference exists:
+    make -C oracle            # builds oracle/_ref/libzrc4_ref.so from
+                              # /root/reference/depends/rc4/rc4_encryption.h
+    python tests/golden/make_golden.py
+
+Every expected output below is produced by the reference class RC4Encryption
+itself (rc4_encryption.h:43-99) through oracle/ref_shim.cpp -- not by the
+restatement under test.  Published vectors (Wikipedia RC4 page; RFC 6229) are
+also recorded verbatim and cross-checked against the reference here.
+
+Outputs (all small):
+  kat.json          published KATs + RFC 6229 keystream offsets
+  edge.json         edge cases: empty / NUL / >256-byte keys, length 0,
+                    split invariance, final states
+  batch_small.npz   64 ragged sessions: random keys 0..300 B, random
+                    pre-advance, ragged lengths and unaligned offsets
+  synth_digests.json  SHA-256 of ciphertext + final states of the synthetic
+                    bench workloads cfg2..cfg5 (full BASELINE sizes)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import hashlib
+import json
+import random
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+import pyoracle  # noqa: E402
+from zsummerx_amd import synth  # noqa: E402
+
+OUT = Path(__file__).resolve().parent
+
+# Published vectors (text copied from the public standards, not the reference)
+WIKI = [("Key", "Plaintext", "BBF316E8D940AF0AD3"),
+        ("Wiki", "pedia", "1021BF0420"),
+        ("Secret", "Attack at dawn", "45A01F645FC35B383552544B9BF5")]
+RFC6229_PUBLISHED = [  # (key hex, offset, keystream hex)
+    ("0102030405", 0, "b2396305f03dc027ccc3524a0a1118a8"),
+    ("0102030405", 4080, "068326a2118416d21f9d04b2cd1ca050"),
+    ("0102030405060708090a0b0c0d0e0f10", 0, "9ac7cc9a609d1ef7b2932899cde41b97"),
+]
+RFC_OFFSETS = [0, 16, 240, 256, 496, 512, 752, 768, 1008, 1024, 1520, 1536,
+               2032, 2048, 3056, 3072, 4080, 4096]
+RFC_KEYS = ["0102030405", "01020304050607", "0102030405060708", "0102030405060708090a",
+            "0102030405060708090a0b0c0d0e0f10",
+            "0102030405060708090a0b0c0d0e0f101112131415161718",
+            "0102030405060708090a0b0c0d0e0f101112131415161718191a1b1c1d1e1f20"]
+
+
+def ref_crypt(key: bytes, data: bytes, splits=None):
+    r = pyoracle.RefRc4(key)
+    if not splits:
+        out = r.encryption(data)
+    else:
+        out, pos = b"", 0
+        for s in splits:
+            out += r.encryption(data[pos:pos + s])
+            pos += s
+    return out, r.state()
+
+
+def st_json(st):
+    sb, x, y = st
+    return {"sbox": sb.hex(), "x": x, "y": y}
+
+
+def gen_kat():
+    kat = {"wikipedia": [], "rfc6229": [], "rfc6229_published": []}
+    for k, p, c in WIKI:
+        out, _ = ref_crypt(k.encode(), p.encode())
+        assert out.hex().upper() == c, (k, out.hex())
+        kat["wikipedia"].append({"key": k.encode().hex(), "plaintext": p.encode().hex(),
+                                 "ciphertext": c.lower()})
+    for khex in RFC_KEYS:
+        ks, _ = ref_crypt(bytes.fromhex(khex), bytes(4112))
+        kat["rfc6229"].append({"key": khex, "offsets": {str(o): ks[o:o + 16].hex()
+                                                        for o in RFC_OFFSETS}})
+    for khex, o, v in RFC6229_PUBLISHED:
+        ks, _ = ref_crypt(bytes.fromhex(khex), bytes(o + 16))
+        assert ks[o:o + 16].hex() == v, (khex, o)
+        kat["rfc6229_published"].append({"key": khex, "offset": o, "keystream": v})
+    return kat
+
+
+def gen_edge():
+    rng = random.Random(7)
+    cases = []
+
+    def add(name, key, data, splits=None):
+        out, st = ref_crypt(key, data, splits)
+        cases.append({"name": name, "key": key.hex(), "data": data.hex(),
+                      "splits": splits, "out": out.hex(), "state": st_json(st)})
+
+    text = bytes(rng.randrange(256) for _ in range(700))
+    add("empty_key", b"", text[:64])
+    add("one_byte_key", b"\x00", text[:64])
+    add("nul_key", b"a\x00b", text[:64])
+    add("nul_key_truncation", b"a", text[:64])
+    add("key_255", bytes(rng.randrange(256) for _ in range(255)), text[:100])
+    add("key_256", bytes(range(256)), text[:100])
+    long_key = bytes(rng.randrange(256) for _ in range(300))
+    add("key_300", long_key, text[:100])
+    add("key_300_prefix256", long_key[:256], text[:100])
+    add("len_0", b"Key", b"")
+    add("len_1", b"Key", text[:1])
+    add("split_3_7", b"Key", text[:10], [3, 7])
+    add("split_whole_10", b"Key", text[:10])
+    add("split_ragged", b"Secret", text, [0, 1, 15, 16, 17, 63, 64, 65, 0, 200, 248])
+    add("wrap_700", b"Wiki", text)
+    # negative length: RC4Encryption::encryption(data, -5) is a no-op
+    r = pyoracle.RefRc4(b"Key")
+    before = r.state()
+    buf = r.encryption(text[:8], -5)
+    assert buf == text[:8] and r.state() == before
+    cases.append({"name": "negative_length_noop", "key": b"Key".hex(), "data": text[:8].hex(),
+                  "length": -5, "out": buf.hex(), "state": st_json(before)})
+    return {"cases": cases}
+
+
+def gen_batch_small():
+    rng = np.random.default_rng(1234)
+    n = 64
+    key_len = rng.integers(0, 301, size=n).astype(np.uint32)
+    key_len[:4] = [0, 1, 256, 300]
+    key_off = np.zeros(n, dtype=np.uint64)
+    key_off[1:] = np.cumsum(key_len[:-1], dtype=np.uint64)
+    keys = rng.integers(0, 256, size=int(key_len.sum()) or 1, dtype=np.uint8)
+    keys[int(key_off[2]):int(key_off[2]) + 8] = 0  # NULs inside a key
+    adv = rng.integers(0, 1001, size=n).astype(np.uint32)
+    length = rng.integers(0, 3001, size=n).astype(np.uint32)
+    length[:16] = [0, 1, 2, 3, 15, 16, 17, 31, 63, 64, 65, 127, 128, 129, 1023, 4096]
+    # unaligned, non-overlapping offsets with random gaps
+    gaps = rng.integers(0, 40, size=n).astype(np.uint64)
+    off = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(gaps[i])
+        off[i] = pos
+        pos += int(length[i])
+    payload_in = rng.integers(0, 256, size=pos + 16, dtype=np.uint8)
+    payload_out = payload_in.copy()
+    states = np.zeros((n, 258), dtype=np.uint8)
+    for i in range(n):
+        k = keys[int(key_off[i]):int(key_off[i]) + int(key_len[i])].tobytes()
+        r = pyoracle.RefRc4(k)
+        r.encryption(bytes(int(adv[i])))
+        a, b = int(off[i]), int(off[i] + length[i])
+        payload_out[a:b] = np.frombuffer(r.encryption(payload_in[a:b].tobytes()), dtype=np.uint8)
+        sb, x, y = r.state()
+        states[i, :256] = np.frombuffer(sb, dtype=np.uint8)
+        states[i, 256], states[i, 257] = x, y
+    np.savez_compressed(OUT / "batch_small.npz", keys=keys, key_off=key_off, key_len=key_len,
+                        adv=adv, off=off, length=length, payload_in=payload_in,
+                        payload_out=payload_out, states=states)
+
+
+def ref_run_workload(w: synth.Workload):
+    """Reference ciphertext + final states for a synthetic workload."""
+    R = pyoracle.ref_lib()
+    sz = R.zrc4_ref_state_size()
+    mem = (C.c_uint8 * (sz * w.n))()
+    base = C.addressof(mem)
+    for i in range(w.n):
+        k = w.keys[16 * i:16 * i + 16].tobytes()
+        R.zrc4_ref_make_sbox(C.c_void_p(base + i * sz), (C.c_uint8 * 16).from_buffer_copy(k), 16)
+    scratch = np.zeros(1000, dtype=np.uint8)
+    zero = np.zeros(w.n, dtype=np.uint64)
+    # pre-advance each state (sid*37)%1000 bytes, then the timed-region payload
+    adv_buf = np.zeros(1000, dtype=np.uint8)
+    R.zrc4_ref_crypt_batch(mem, C.c_void_p(adv_buf.ctypes.data), C.c_void_p(zero.ctypes.data),
+                           C.c_void_p(w.adv.ctypes.data), w.n)
+    del scratch
+    out = w.payload.copy()
+    R.zrc4_ref_crypt_batch(mem, C.c_void_p(out.ctypes.data), C.c_void_p(w.off.ctypes.data),
+                           C.c_void_p(w.length.ctypes.data), w.n)
+    states = np.zeros((w.n, 258), dtype=np.uint8)
+    sb = (C.c_uint8 * 256)()
+    x, y = C.c_uint8(), C.c_uint8()
+    for i in range(w.n):
+        R.zrc4_ref_get_state(C.c_void_p(base + i * sz), sb, C.byref(x), C.byref(y))
+        states[i, :256] = np.frombuffer(bytes(sb), dtype=np.uint8)
+        states[i, 256], states[i, 257] = x.value, y.value
+    return out, states
+
+
+def gen_synth_digests():
+    res = {}
+    for name, (S, L) in synth.CONFIGS.items():
+        w = synth.make(0, S, L, threads=8)
+        out, states = ref_run_workload(w)
+        res[name] = {"sessions": S, "L": L,
+                     "payload_in_sha256": hashlib.sha256(w.payload.tobytes()).hexdigest(),
+                     "ciphertext_sha256": hashlib.sha256(out.tobytes()).hexdigest(),
+                     "states_sha256": hashlib.sha256(states.tobytes()).hexdigest(),
+                     "first_session_ct16": out[:16].tobytes().hex(),
+                     "last_session_state": states[-1].tobytes().hex()}
+        print(name, res[name]["ciphertext_sha256"][:16], flush=True)
+    return res
+
+
+def main():
+    if pyoracle.ref_lib() is None:
+        sys.exit("oracle/_ref/libzrc4_ref.so missing: run `make -C oracle` with /root/reference present")
+    (OUT / "kat.json").write_text(json.dumps(gen_kat(), indent=1) + "\n")
+    (OUT / "edge.json").write_text(json.dumps(gen_edge(), indent=1) + "\n")
+    gen_batch_small()
+    if "--no-synth" not in sys.argv:
+        (OUT / "synth_digests.json").write_text(json.dumps(gen_synth_digests(), indent=1) + "\n")
+    print("golden fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()

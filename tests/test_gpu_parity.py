@@ -1,0 +1,218 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the golden
+fixtures made by the real reference header, against the oracle on seeded
+inputs, and at BASELINE.json's full sizes against the reference's SHA-256
+digests.  Bit-exact everywhere (integer/byte work).  Run with -m gpu on a
+MI355X."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import pyoracle
+from zsummerx_amd import Context, RC4Encryption, ZRC4Error, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx(built):
+    c = Context(0, 4096)
+    yield c
+    c.close()
+
+
+def state_of(ctx, slot):
+    sb, x, y = ctx.get_state(slot)
+    return sb.hex(), x, y
+
+
+# ---------------------------------------------------------------- KATs / edges
+def test_kats_single_stream(ctx, kat):
+    for i, v in enumerate(kat["wikipedia"]):
+        ctx.make_sbox(i, bytes.fromhex(v["key"]))
+        data = bytearray.fromhex(v["plaintext"])
+        ctx.encryption(i, data, len(data))
+        assert data.hex() == v["ciphertext"]
+    for i, v in enumerate(kat["rfc6229"]):
+        ctx.make_sbox(10 + i, bytes.fromhex(v["key"]))
+        ks = bytearray(4112)
+        ctx.encryption(10 + i, ks, len(ks))
+        for o, want in v["offsets"].items():
+            assert ks[int(o):int(o) + 16].hex() == want
+
+
+def test_edge_cases(ctx, edge):
+    for i, c in enumerate(edge):
+        slot = 100 + i
+        ctx.make_sbox(slot, bytes.fromhex(c["key"]))
+        data = bytearray.fromhex(c["data"])
+        if "length" in c:
+            ctx.encryption(slot, data, c["length"])
+        elif c["splits"]:
+            pos = 0
+            for s in c["splits"]:
+                part = bytearray(data[pos:pos + s])
+                ctx.encryption(slot, part, len(part))
+                data[pos:pos + s] = part
+                pos += s
+        else:
+            ctx.encryption(slot, data, len(data))
+        assert data.hex() == c["out"], c["name"]
+        assert state_of(ctx, slot) == (c["state"]["sbox"], c["state"]["x"], c["state"]["y"]), c["name"]
+
+
+def test_rc4encryption_mirror_class(built, kat):
+    v = kat["wikipedia"][2]
+    r = RC4Encryption()
+    r.makeSBox(bytes.fromhex(v["key"]).decode())
+    data = bytearray.fromhex(v["plaintext"])
+    r.encryption(data, len(data))
+    assert data.hex() == v["ciphertext"]
+    r.encryption(data, 0)            # no-op
+    r.encryption(data, -3)           # no-op (reference: length <= 0)
+
+
+# ----------------------------------------------------------- batched, ragged
+def _seed_batch(ctx, b, ids):
+    n = b["key_len"].size
+    ctx.ksa_host([b["keys"][int(o):int(o) + int(l)].tobytes() for o, l in zip(b["key_off"], b["key_len"])],
+                 ids=ids)
+    scratch = np.zeros(1000 * n, dtype=np.uint8)
+    ctx.crypt_host(scratch, np.arange(n, dtype=np.uint64) * 1000, b["adv"], ids=ids)
+
+
+def _check_batch(ctx, b, ids, pay):
+    assert np.array_equal(pay, b["payload_out"])
+    for i in range(b["key_len"].size):
+        sb, x, y = ctx.get_state(int(ids[i]) if ids is not None else i)
+        assert sb == b["states"][i, :256].tobytes() and (x, y) == tuple(b["states"][i, 256:]), i
+
+
+def test_batch_small_identity_ids(ctx, batch_small):
+    b = batch_small
+    _seed_batch(ctx, b, None)
+    pay = b["payload_in"].copy()
+    ctx.crypt_host(pay, b["off"], b["length"])
+    _check_batch(ctx, b, None, pay)
+
+
+def test_batch_small_scattered_ids(ctx, batch_small):
+    """Arbitrary slot ids (gather/scatter path): a permutation across groups."""
+    b = batch_small
+    n = b["key_len"].size
+    ids = (np.random.default_rng(3).permutation(4096)[:n]).astype(np.uint32)
+    _seed_batch(ctx, b, ids)
+    pay = b["payload_in"].copy()
+    ctx.crypt_host(pay, b["off"], b["length"], ids=ids)
+    _check_batch(ctx, b, ids, pay)
+
+
+def test_batch_whole_group_ids(ctx, batch_small):
+    """ids given but exactly an aligned 256-slot group -> coalesced fast path."""
+    rng = np.random.default_rng(9)
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(256)]
+    ids = np.arange(512, 768, dtype=np.uint32)
+    ctx.ksa_host(keys, ids=ids)
+    L = np.array([int(v) for v in rng.integers(0, 700, 256)], dtype=np.uint32)
+    off = np.concatenate([[0], np.cumsum(L[:-1])]).astype(np.uint64)
+    pay = rng.integers(0, 256, int(L.sum()) + 1, dtype=np.uint8)
+    want = pay.copy()
+    ctx.crypt_host(pay, off, L, ids=ids)
+    for i in range(256):
+        a, z = int(off[i]), int(off[i] + L[i])
+        want[a:z] = np.frombuffer(pyoracle.Rc4(keys[i]).encryption(want[a:z].tobytes()), np.uint8)
+    assert np.array_equal(pay, want)
+
+
+def test_split_invariance_batched(ctx):
+    """N calls of a few bytes == one call of the sum (keystream continues)."""
+    rng = np.random.default_rng(4)
+    n = 300
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(n)]
+    ctx.ksa_host(keys)
+    total = 777
+    data = rng.integers(0, 256, n * total, dtype=np.uint8)
+    want = data.copy()
+    for i in range(n):
+        want[i * total:(i + 1) * total] = np.frombuffer(
+            pyoracle.Rc4(keys[i]).encryption(data[i * total:(i + 1) * total].tobytes()), np.uint8)
+    pos = 0
+    for step in [1, 3, 16, 17, 64, 100, 0, 200, 376]:
+        off = (np.arange(n, dtype=np.uint64) * total + pos).astype(np.uint64)
+        ctx.crypt_host(data, off, np.full(n, step, dtype=np.uint32))
+        pos += step
+    assert pos == total
+    assert np.array_equal(data, want)
+
+
+def test_state_roundtrip_and_import(ctx):
+    r = pyoracle.Rc4(b"roundtrip")
+    r.encryption(bytes(333))
+    sb, x, y = r.state()
+    ctx.set_state(7, sb, x, y)
+    assert ctx.get_state(7) == (sb, x, y)
+    data = bytearray(range(200))
+    want = r.encryption(bytes(data))
+    ctx.encryption(7, data, len(data))
+    assert bytes(data) == want
+
+
+def test_slot_out_of_range_is_reported(ctx, torch_cuda):
+    torch = torch_cuda
+    with pytest.raises(ZRC4Error):
+        ctx.make_sbox(ctx.capacity, b"k")
+    ids = torch.tensor([0, ctx.capacity + 5], dtype=torch.int32, device="cuda")
+    pay = torch.zeros(32, dtype=torch.uint8, device="cuda")
+    off = torch.tensor([0, 16], dtype=torch.int64, device="cuda")
+    ln = torch.tensor([16, 16], dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    ctx.crypt(pay, off, ln, ids=ids, stream=s)
+    with pytest.raises(ZRC4Error) as ei:
+        ctx.sync(s)
+    assert ei.value.code == -5
+    ctx.sync(s)  # latch cleared
+
+
+# ------------------------------------------------ full BASELINE-size configs
+def _device_workload(ctx, w, torch):
+    dev = "cuda"
+    t = lambda a: torch.from_numpy(a.view(np.uint8) if a.dtype == np.uint8 else a).to(dev)
+    s = torch.cuda.current_stream()
+    ctx.ksa(t(w.key_len.view(np.int32)), t(w.key_off.view(np.int64)), t(w.keys), stream=s)
+    scratch = torch.zeros(1000, dtype=torch.uint8, device=dev)
+    zero = torch.zeros(w.n, dtype=torch.int64, device=dev)
+    ctx.crypt(scratch, zero, t(w.adv.view(np.int32)), stream=s)   # pre-advance
+    pay = t(w.payload)
+    ctx.crypt(pay, t(w.off.view(np.int64)), t(w.length.view(np.int32)), stream=s)
+    ctx.sync(s)
+    return pay.cpu().numpy()
+
+
+def _states_digest(ctx, n):
+    h = hashlib.sha256()
+    for i in range(n):
+        sb, x, y = ctx.get_state(i)
+        h.update(sb + bytes([x, y]))
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4", "cfg5"])
+def test_baseline_configs_bit_exact(cfg, synth_digests, torch_cuda, built):
+    S, L = synth.CONFIGS[cfg]
+    d = synth_digests[cfg]
+    w = synth.make(0, S, L, threads=8)
+    with Context(0, S) as c:
+        out = _device_workload(c, w, torch_cuda)
+        assert hashlib.sha256(out.tobytes()).hexdigest() == d["ciphertext_sha256"], cfg
+        if S <= 65536:
+            assert _states_digest(c, S) == d["states_sha256"], cfg
+        else:
+            sb, x, y = c.get_state(S - 1)
+            assert (sb + bytes([x, y])).hex() == d["last_session_state"]

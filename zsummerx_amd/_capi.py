@@ -1,0 +1,85 @@
+"""ctypes binding of include/zrc4.h (the C-ABI a maintainer's FFI would bind).
+
+No fallback: if libzrc4.so is missing or no gfx950 device is present, the
+calls fail loudly (ZRC4Error), they never drop to a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "libzrc4.so"
+
+ZRC4_OK = 0
+ERRORS = {
+    -1: "ZRC4_ERR_INVALID_ARG",
+    -2: "ZRC4_ERR_NO_DEVICE",
+    -3: "ZRC4_ERR_OUT_OF_MEMORY",
+    -4: "ZRC4_ERR_LAUNCH",
+    -5: "ZRC4_ERR_SLOT_RANGE",
+    -6: "ZRC4_ERR_HIP",
+}
+
+# (name, restype, argtypes) for every symbol declared in include/zrc4.h
+_P = C.c_void_p
+_U8P = C.POINTER(C.c_uint8)
+SIGNATURES = [
+    ("zrc4_create", C.c_int, [C.POINTER(_P), C.c_int, C.c_uint32]),
+    ("zrc4_destroy", C.c_int, [_P]),
+    ("zrc4_capacity", C.c_uint32, [_P]),
+    ("zrc4_ksa", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
+    ("zrc4_crypt", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
+    ("zrc4_ksa_host", C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, C.c_uint32]),
+    ("zrc4_crypt_host", C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, C.c_uint32]),
+    ("zrc4_make_sbox", C.c_int, [_P, C.c_uint32, _P, C.c_size_t]),
+    ("zrc4_encryption", C.c_int, [_P, C.c_uint32, _P, C.c_int]),
+    ("zrc4_sync", C.c_int, [_P, _P]),
+    ("zrc4_get_state", C.c_int, [_P, C.c_uint32, _U8P, _U8P, _U8P]),
+    ("zrc4_set_state", C.c_int, [_P, C.c_uint32, _U8P, C.c_uint8, C.c_uint8]),
+    ("zrc4_strerror", C.c_char_p, [C.c_int]),
+    ("zrc4_version", C.c_char_p, []),
+]
+
+
+class ZRC4Error(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        name = ERRORS.get(code, str(code))
+        msg = f"{name}: {_strerror(code)}"
+        super().__init__(f"{what}: {msg}" if what else msg)
+
+
+_lib = None
+
+
+def load(path: Path | str | None = None) -> C.CDLL:
+    """Load libzrc4.so and declare every prototype.  Raises if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise FileNotFoundError(
+            f"{p} not built: run `python -m zsummerx_amd.build` (hipcc --offload-arch=gfx950); "
+            "there is no CPU fallback for the RC4 path")
+    lib = C.CDLL(str(p))
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _strerror(code: int) -> str:
+    try:
+        return load().zrc4_strerror(code).decode()
+    except Exception:  # library itself missing
+        return "unknown"
+
+
+def check(code: int, what: str = "") -> None:
+    if code != ZRC4_OK:
+        raise ZRC4Error(code, what)

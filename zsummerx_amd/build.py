@@ -1,0 +1,73 @@
+"""In-tree build of the native pieces (no JIT cache, so the .so files travel to
+the GPU box with the repo snapshot).
+
+  libzrc4.so        C-ABI product library: HIP kernels for gfx950 + host side
+  libzrc4_synth.so  synthetic workload generator (bench/tests input data)
+  oracle/           CPU restatement (+ oracle/_ref when /root/reference exists)
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = ROOT / "build"
+ARCH = "gfx950"
+
+LIB = PKG / "libzrc4.so"
+SYNTH = PKG / "libzrc4_synth.so"
+
+HIP_SOURCES = [CSRC / "zrc4.hip"]
+HIP_DEPS = HIP_SOURCES + [CSRC / "zrc4_kernels.hpp", ROOT / "include" / "zrc4.h"]
+
+
+def _hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the zrc4 HIP library cannot be built")
+
+
+def _stale(out: Path, deps) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def build_lib(force: bool = False, extra_flags=()) -> Path:
+    if force or _stale(LIB, HIP_DEPS):
+        BUILD.mkdir(exist_ok=True)
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wall", f"-I{ROOT / 'include'}", f"-save-temps={BUILD}/", *extra_flags,
+               "-o", str(LIB), *map(str, HIP_SOURCES)]
+        subprocess.run(cmd, check=True, cwd=BUILD)
+    return LIB
+
+
+def build_synth(force: bool = False) -> Path:
+    src = CSRC / "synth.cpp"
+    if force or _stale(SYNTH, [src]):
+        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", str(SYNTH), str(src)]
+        subprocess.run(cmd, check=True)
+    return SYNTH
+
+
+def build_oracle() -> None:
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
+
+
+def build_all(force: bool = False) -> None:
+    build_lib(force)
+    build_synth(force)
+    build_oracle()
+
+
+if __name__ == "__main__":
+    import sys
+    build_all(force="--force" in sys.argv)
+    print("built", LIB, SYNTH)

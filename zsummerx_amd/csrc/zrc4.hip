@@ -1,0 +1,323 @@
+// zrc4.hip -- C-ABI implementation (include/zrc4.h) over the gfx950 kernels.
+//
+// Host side of the drop-in for RC4Encryption (depends/rc4/rc4_encryption.h:43-99).
+// The device arena replaces the by-value RC4Encryption members of TcpSession
+// (include/zsummerX/frame/session.h:115-116); see INTEGRATION.md.
+#include "zrc4.h"
+#include "zrc4_kernels.hpp"
+
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+#include <new>
+
+struct zrc4_ctx {
+    int device;
+    uint32_t capacity;      // multiple of 256
+    uint8_t *arena;         // capacity/256 groups x 64 KiB S-box images
+    uint16_t *xy;           // per slot: x | y << 8
+    uint32_t *err;          // latched device-side fault bits
+    // staging for the *_host entry points (grown on demand)
+    uint8_t *d_stage;
+    size_t d_stage_bytes;
+    uint8_t *h_stage;       // pinned
+    size_t h_stage_bytes;
+    hipStream_t stream;     // private stream for the host entry points
+};
+
+namespace {
+
+int hip_err(hipError_t e) { return e == hipSuccess ? ZRC4_OK : ZRC4_ERR_HIP; }
+
+#define ZRC4_TRY(expr)                          \
+    do {                                        \
+        hipError_t e_ = (expr);                 \
+        if (e_ != hipSuccess) return ZRC4_ERR_HIP; \
+    } while (0)
+
+int set_device(const zrc4_ctx *c)
+{
+    return hip_err(hipSetDevice(c->device));
+}
+
+int grow_stage(zrc4_ctx *c, size_t bytes)
+{
+    if (bytes <= c->d_stage_bytes && bytes <= c->h_stage_bytes) return ZRC4_OK;
+    size_t want = 1u << 20;
+    while (want < bytes) want <<= 1;
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    c->d_stage = nullptr;
+    c->h_stage = nullptr;
+    c->d_stage_bytes = c->h_stage_bytes = 0;
+    if (hipMalloc(&c->d_stage, want) != hipSuccess) return ZRC4_ERR_OUT_OF_MEMORY;
+    if (hipHostMalloc(&c->h_stage, want, hipHostMallocDefault) != hipSuccess)
+        return ZRC4_ERR_OUT_OF_MEMORY;
+    c->d_stage_bytes = c->h_stage_bytes = want;
+    return ZRC4_OK;
+}
+
+size_t align16(size_t v) { return (v + 15u) & ~(size_t)15u; }
+
+int launch_crypt(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_t *off,
+                 const uint32_t *len, uint32_t n, hipStream_t s)
+{
+    if (n == 0) return ZRC4_OK;
+    if (!ids && n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
+    hipLaunchKernelGGL(zrc4::crypt_kernel, dim3(grid), dim3(zrc4::kGroup), 0, s, c->arena,
+                       c->xy, ids, payload, off, len, n, c->capacity, c->err);
+    return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
+}
+
+int launch_ksa(zrc4_ctx *c, const uint32_t *ids, const uint8_t *keys, const uint64_t *key_off,
+               const uint32_t *key_len, uint32_t n, hipStream_t s)
+{
+    if (n == 0) return ZRC4_OK;
+    if (!ids && n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
+    hipLaunchKernelGGL(zrc4::ksa_kernel, dim3(grid), dim3(zrc4::kGroup), 0, s, c->arena, c->xy,
+                       ids, keys, key_off, key_len, n, c->capacity, c->err);
+    return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
+}
+
+int check_err(zrc4_ctx *c, hipStream_t s)
+{
+    uint32_t h = 0;
+    ZRC4_TRY(hipMemcpyAsync(&h, c->err, sizeof(h), hipMemcpyDeviceToHost, s));
+    ZRC4_TRY(hipStreamSynchronize(s));
+    if (h) {
+        ZRC4_TRY(hipMemsetAsync(c->err, 0, sizeof(uint32_t), s));
+        ZRC4_TRY(hipStreamSynchronize(s));
+        return ZRC4_ERR_SLOT_RANGE;
+    }
+    return ZRC4_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zrc4_create(zrc4_ctx **out, int device, uint32_t capacity)
+{
+    if (!out || capacity == 0) return ZRC4_ERR_INVALID_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ZRC4_ERR_NO_DEVICE;
+    if (device < 0 || device >= ndev) return ZRC4_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return ZRC4_ERR_NO_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ZRC4_ERR_NO_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return ZRC4_ERR_NO_DEVICE;
+
+    zrc4_ctx *c = new (std::nothrow) zrc4_ctx();
+    if (!c) return ZRC4_ERR_OUT_OF_MEMORY;
+    c->device = device;
+    const uint64_t cap = ((uint64_t)capacity + 255u) & ~(uint64_t)255u;
+    if (cap > 0xFFFFFF00ull) { delete c; return ZRC4_ERR_INVALID_ARG; }
+    c->capacity = (uint32_t)cap;
+    const size_t groups = c->capacity / zrc4::kGroup;
+    bool ok = hipMalloc(&c->arena, groups * (size_t)zrc4::kGroupBytes) == hipSuccess &&
+              hipMalloc(&c->xy, (size_t)c->capacity * sizeof(uint16_t)) == hipSuccess &&
+              hipMalloc(&c->err, sizeof(uint32_t)) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) { zrc4_destroy(c); return ZRC4_ERR_OUT_OF_MEMORY; }
+    // Fresh slots hold the reference's empty-key state: identity box, x = y = 0
+    // (what makeSBox("") produces, rc4_encryption.h:48-53).
+    hipLaunchKernelGGL(zrc4::identity_kernel, dim3((unsigned)groups), dim3(zrc4::kGroup), 0,
+                       c->stream, c->arena);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemsetAsync(c->xy, 0, (size_t)c->capacity * sizeof(uint16_t), c->stream) != hipSuccess ||
+        hipMemsetAsync(c->err, 0, sizeof(uint32_t), c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        zrc4_destroy(c);
+        return ZRC4_ERR_HIP;
+    }
+    *out = c;
+    return ZRC4_OK;
+}
+
+int zrc4_destroy(zrc4_ctx *c)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->arena) (void)hipFree(c->arena);
+    if (c->xy) (void)hipFree(c->xy);
+    if (c->err) (void)hipFree(c->err);
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return ZRC4_OK;
+}
+
+uint32_t zrc4_capacity(const zrc4_ctx *c) { return c ? c->capacity : 0u; }
+
+int zrc4_ksa(zrc4_ctx *c, const uint32_t *ids, const uint8_t *keys, const uint64_t *key_off,
+             const uint32_t *key_len, uint32_t n, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n && (!key_len || !key_off)) return ZRC4_ERR_INVALID_ARG;
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_ksa(c, ids, keys, key_off, key_len, n, (hipStream_t)stream);
+}
+
+int zrc4_crypt(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_t *off,
+               const uint32_t *len, uint32_t n, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n && (!payload || !off || !len)) return ZRC4_ERR_INVALID_ARG;
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_crypt(c, ids, payload, off, len, n, (hipStream_t)stream);
+}
+
+int zrc4_sync(zrc4_ctx *c, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    int rc = set_device(c);
+    if (rc) return rc;
+    ZRC4_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return check_err(c, (hipStream_t)stream);
+}
+
+int zrc4_ksa_host(zrc4_ctx *c, const uint32_t *ids, const uint8_t *keys, size_t keys_bytes,
+                  const uint64_t *key_off, const uint32_t *key_len, uint32_t n)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n == 0) return ZRC4_OK;
+    if (!key_off || !key_len || (keys_bytes && !keys)) return ZRC4_ERR_INVALID_ARG;
+    for (uint32_t i = 0; i < n; ++i)
+        if (key_len[i] && (key_off[i] > keys_bytes || key_len[i] > keys_bytes - key_off[i]))
+            return ZRC4_ERR_INVALID_ARG;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const size_t o_ids = 0, s_ids = ids ? align16((size_t)n * 4) : 0;
+    const size_t o_off = o_ids + s_ids, s_off = align16((size_t)n * 8);
+    const size_t o_len = o_off + s_off, s_len = align16((size_t)n * 4);
+    const size_t o_key = o_len + s_len, total = o_key + align16(keys_bytes ? keys_bytes : 1);
+    if ((rc = grow_stage(c, total))) return rc;
+    if (ids) memcpy(c->h_stage + o_ids, ids, (size_t)n * 4);
+    memcpy(c->h_stage + o_off, key_off, (size_t)n * 8);
+    memcpy(c->h_stage + o_len, key_len, (size_t)n * 4);
+    if (keys_bytes) memcpy(c->h_stage + o_key, keys, keys_bytes);
+    ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
+    rc = launch_ksa(c, ids ? (const uint32_t *)(c->d_stage + o_ids) : nullptr,
+                    c->d_stage + o_key, (const uint64_t *)(c->d_stage + o_off),
+                    (const uint32_t *)(c->d_stage + o_len), n, c->stream);
+    if (rc) return rc;
+    return check_err(c, c->stream);
+}
+
+int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t payload_bytes,
+                    const uint64_t *off, const uint32_t *len, uint32_t n)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n == 0) return ZRC4_OK;
+    if (!off || !len || (payload_bytes && !payload)) return ZRC4_ERR_INVALID_ARG;
+    for (uint32_t i = 0; i < n; ++i)
+        if (len[i] && (off[i] > payload_bytes || len[i] > payload_bytes - off[i]))
+            return ZRC4_ERR_INVALID_ARG;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const size_t o_ids = 0, s_ids = ids ? align16((size_t)n * 4) : 0;
+    const size_t o_off = o_ids + s_ids, s_off = align16((size_t)n * 8);
+    const size_t o_len = o_off + s_off, s_len = align16((size_t)n * 4);
+    const size_t o_pay = o_len + s_len, total = o_pay + align16(payload_bytes ? payload_bytes : 1);
+    if ((rc = grow_stage(c, total))) return rc;
+    if (ids) memcpy(c->h_stage + o_ids, ids, (size_t)n * 4);
+    memcpy(c->h_stage + o_off, off, (size_t)n * 8);
+    memcpy(c->h_stage + o_len, len, (size_t)n * 4);
+    if (payload_bytes) memcpy(c->h_stage + o_pay, payload, payload_bytes);
+    ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
+    rc = launch_crypt(c, ids ? (const uint32_t *)(c->d_stage + o_ids) : nullptr,
+                      c->d_stage + o_pay, (const uint64_t *)(c->d_stage + o_off),
+                      (const uint32_t *)(c->d_stage + o_len), n, c->stream);
+    if (rc) return rc;
+    if (payload_bytes)
+        ZRC4_TRY(hipMemcpyAsync(c->h_stage + o_pay, c->d_stage + o_pay, payload_bytes,
+                                hipMemcpyDeviceToHost, c->stream));
+    rc = check_err(c, c->stream);
+    if (rc) return rc;
+    if (payload_bytes) memcpy(payload, c->h_stage + o_pay, payload_bytes);
+    return ZRC4_OK;
+}
+
+int zrc4_make_sbox(zrc4_ctx *c, uint32_t id, const uint8_t *key, size_t keylen)
+{
+    if (!c || (keylen && !key)) return ZRC4_ERR_INVALID_ARG;
+    if (id >= c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    // Only the first 256 key bytes can reach the S-box (the KSA runs i = 0..255
+    // and reads key[i % len], rc4_encryption.h:60-70).
+    const size_t kl = keylen > 256 ? 256 : keylen;
+    const uint64_t ko = 0;
+    const uint32_t kl32 = (uint32_t)kl;
+    return zrc4_ksa_host(c, &id, key, kl, &ko, &kl32, 1);
+}
+
+int zrc4_encryption(zrc4_ctx *c, uint32_t id, uint8_t *data, int length)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (id >= c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    if (length <= 0) return ZRC4_OK;  // for (i = 0; i < length; ...) never runs (:81)
+    if (!data) return ZRC4_ERR_INVALID_ARG;
+    const uint64_t o = 0;
+    const uint32_t l = (uint32_t)length;
+    return zrc4_crypt_host(c, &id, data, (size_t)length, &o, &l, 1);
+}
+
+int zrc4_get_state(zrc4_ctx *c, uint32_t id, uint8_t sbox[256], uint8_t *x, uint8_t *y)
+{
+    if (!c || !sbox || !x || !y) return ZRC4_ERR_INVALID_ARG;
+    if (id >= c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const uint8_t *img = c->arena + (size_t)(id >> 8) * zrc4::kGroupBytes;
+    const uint32_t j = id & 255u, w = j >> 6, l = j & 63u;
+    const uint32_t col = ((l & 31u) << 2) | (l >> 5) | ((w & 1u) << 1) | ((w >> 1) << 7);
+    ZRC4_TRY(hipMemcpy2DAsync(sbox, 1, img + col, 256, 1, 256, hipMemcpyDeviceToHost, c->stream));
+    uint16_t v = 0;
+    ZRC4_TRY(hipMemcpyAsync(&v, c->xy + id, 2, hipMemcpyDeviceToHost, c->stream));
+    ZRC4_TRY(hipStreamSynchronize(c->stream));
+    *x = (uint8_t)(v & 255u);
+    *y = (uint8_t)(v >> 8);
+    return ZRC4_OK;
+}
+
+int zrc4_set_state(zrc4_ctx *c, uint32_t id, const uint8_t sbox[256], uint8_t x, uint8_t y)
+{
+    if (!c || !sbox) return ZRC4_ERR_INVALID_ARG;
+    if (id >= c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    int rc = set_device(c);
+    if (rc) return rc;
+    uint8_t *img = c->arena + (size_t)(id >> 8) * zrc4::kGroupBytes;
+    const uint32_t j = id & 255u, w = j >> 6, l = j & 63u;
+    const uint32_t col = ((l & 31u) << 2) | (l >> 5) | ((w & 1u) << 1) | ((w >> 1) << 7);
+    uint8_t tmp[258];
+    memcpy(tmp, sbox, 256);
+    const uint16_t v = (uint16_t)(x | (y << 8));
+    ZRC4_TRY(hipMemcpy2DAsync(img + col, 256, tmp, 1, 1, 256, hipMemcpyHostToDevice, c->stream));
+    ZRC4_TRY(hipMemcpyAsync(c->xy + id, &v, 2, hipMemcpyHostToDevice, c->stream));
+    ZRC4_TRY(hipStreamSynchronize(c->stream));
+    return ZRC4_OK;
+}
+
+const char *zrc4_strerror(int code)
+{
+    switch (code) {
+    case ZRC4_OK: return "ok";
+    case ZRC4_ERR_INVALID_ARG: return "invalid argument";
+    case ZRC4_ERR_NO_DEVICE: return "no usable gfx950 (MI355X) HIP device";
+    case ZRC4_ERR_OUT_OF_MEMORY: return "device or pinned memory allocation failed";
+    case ZRC4_ERR_LAUNCH: return "kernel launch failed";
+    case ZRC4_ERR_SLOT_RANGE: return "slot id out of range (>= capacity)";
+    case ZRC4_ERR_HIP: return "HIP runtime error";
+    default: return "unknown zrc4 error";
+    }
+}
+
+const char *zrc4_version(void) { return "zrc4-mi355x 0.1 (gfx950)"; }
+
+}  // extern "C"
