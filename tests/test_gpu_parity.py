@@ -62,6 +62,7 @@ def test_edge_cases(ctx, edge):
                 ctx.encryption(slot, part, len(part))
                 data[pos:pos + s] = part
                 pos += s
+            data = data[:pos]
         else:
             ctx.encryption(slot, data, len(data))
         assert data.hex() == c["out"], c["name"]

@@ -59,6 +59,15 @@ def load(path: Path | str | None = None) -> C.CDLL:
     if _lib is not None and path is None:
         return _lib
     p = Path(path) if path else LIB_PATH
+    # One HIP runtime per process: torch ships its own libamdhip64 (same SONAME
+    # libamdhip64.so.7 as /opt/rocm's).  If libzrc4 were loaded first, a later
+    # `import torch` would map a SECOND runtime and torch.cuda would see no
+    # device.  Importing torch first makes libzrc4 bind to the runtime torch
+    # already mapped.  Plain C/C++ users (no torch) get /opt/rocm's via RUNPATH.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not p.exists():
         raise FileNotFoundError(
             f"{p} not built: run `python -m zsummerx_amd.build` (hipcc --offload-arch=gfx950); "
