@@ -73,38 +73,44 @@ __device__ __forceinline__ void scatter_column(uint8_t *arena, uint32_t slot,
 }
 
 // ---------------------------------------------------------------------------
-// One PRGA step (rc4_encryption.h:83-88) on 16-bit LDS addresses.
-// Loop state between steps:
-//   xa = address of S[x]        (x = the last index used)
+// PRGA (rc4_encryption.h:81-89) on 16-bit LDS addresses.
+//
+// Lane state (all addresses are (index << 8) | col, bytes 2-3 zero):
+//   x0 = address of S[x]  where x is the NEXT index to use (stored x + 1)
+//   a0 = S[x]             (already read)
 //   ya = address of S[y]
-//   an = S[x+1] as it will be seen by the next step (prefetched one step
-//        early, forwarded from this step's S[y] = a write when y == x+1)
-// The next-x read is issued before this step's two writes, so the only
-// LDS round trip on the byte-to-byte chain is the S[y] read.
+//   ta = col in byte 0, scratch index in byte 1 (hand-written path only)
+//
+// Per byte the LDS ops are issued in the order
+//     b = S[y+a] ; S[y] = a ; p = S[x+1] ; S[x] = b ; k = S[a+b]
+// Reading S[x+1] after the S[y] = a write needs no forwarding (the S[x] = b
+// write goes to x != x+1), and the b -> S[x] = b wait no longer gates the
+// next byte, so the byte-to-byte chain holds one LDS round trip (b and p are
+// in flight together).  Swapping the reference's write order (S[x] = b then
+// S[y] = a, :86-87) is exact: the two only collide when x == y, and then
+// b == a.
 // ---------------------------------------------------------------------------
 struct Rc4Lane {
-    uint32_t xa, ya, an, col;
+    uint32_t x0, a0, ya, ta, x1, col;
 };
 
+// Portable C step with the same state layout (head/tail bytes, 16-B chunks).
 __device__ __forceinline__ uint32_t prga_step(uint8_t *S, Rc4Lane &st)
 {
-    const uint32_t xa = (st.xa + 256u) & 0xFFFFu;     // x = (u8)(x+1)
-    const uint32_t a = st.an;                          // a = S[x]
-    const uint32_t ya = (st.ya + (a << 8)) & 0xFFFFu;  // y = (u8)(y+a)
-    const uint32_t b = S[ya];                          // b = S[y]
-    const uint32_t xn = (xa + 256u) & 0xFFFFu;
-    const uint32_t p = S[xn];                          // prefetch S[x+1]
-    S[xa] = (uint8_t)b;                                // S[x] = b
-    S[ya] = (uint8_t)a;                                // S[y] = a
-    const uint32_t ta = (((a + b) << 8) | st.col) & 0xFFFFu;
-    const uint32_t k = S[ta];                          // S[(u8)(a+b)]
-    st.an = (xn == ya) ? a : p;
-    st.xa = xa;
+    const uint32_t a = st.a0;
+    const uint32_t ya = (st.ya & 0xFFu) | ((st.ya + (a << 8)) & 0xFF00u);  // y = (u8)(y+a)
+    const uint32_t b = S[ya];                                                // b = S[y]
+    S[ya] = (uint8_t)a;                                                      // S[y] = a
+    const uint32_t xn = (st.x0 & 0xFFu) | ((st.x0 + 256u) & 0xFF00u);
+    const uint32_t p = S[xn];                                                // next a
+    S[st.x0] = (uint8_t)b;                                                   // S[x] = b
+    const uint32_t k = S[(((a + b) << 8) & 0xFF00u) | st.col];               // S[(u8)(a+b)]
+    st.a0 = p;
+    st.x0 = xn;
     st.ya = ya;
     return k;
 }
 
-// 4 keystream bytes packed little-endian into one dword.
 __device__ __forceinline__ uint32_t prga_word(uint8_t *S, Rc4Lane &st)
 {
     const uint32_t k0 = prga_step(S, st);
@@ -123,9 +129,81 @@ __device__ __forceinline__ uint4 xor16(uint8_t *S, Rc4Lane &st, uint4 v)
     return v;
 }
 
+// Hand-written gfx950 step.  Each index update is ONE SDWA add that rewrites
+// byte 1 of an address register in place (dst_sel:BYTE_1, UNUSED_PRESERVE):
+// the mod-256 wrap is free and col (byte 0) is untouched.  The keystream byte
+// of step s is XORed into its payload byte at the end of step s+1 (its read
+// is retired by step s+1's waits) with one SDWA xor on that byte lane.
+// (ds_read_u8_d16_hi does NOT preserve the low half on gfx950 -- measured --
+// so keystream bytes are not packed through d16 loads.)
+#define ZRC4_CORE(XC, XN, A, P, K)                                                               \
+    "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
+    "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
+    "ds_read_u8 %[b], %[ya]\n\t"                                                                 \
+    "ds_write_b8 %[ya], %[" #A "]\n\t"                                                           \
+    "v_add_u32_sdwa %[" #XN "], 1, %[" #XC "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "        \
+    "src0_sel:DWORD src1_sel:BYTE_1\n\t"                                                         \
+    "ds_read_u8 %[" #P "], %[" #XN "]\n\t"                                                       \
+    "s_waitcnt lgkmcnt(2)\n\t"                                                                   \
+    "ds_write_b8 %[" #XC "], %[b]\n\t"                                                           \
+    "v_add_u32_sdwa %[ta], %[" #A "], %[b] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "           \
+    "src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"                                                        \
+    "ds_read_u8 %[" #K "], %[ta]\n\t"                                                            \
+    "s_waitcnt lgkmcnt(2)\n\t"
+
+#define ZRC4_XOR(D, SEL, K)                                                                      \
+    "v_xor_b32_sdwa %[" #D "], %[" #D "], %[" #K "] dst_sel:" #SEL                               \
+    " dst_unused:UNUSED_PRESERVE src0_sel:" #SEL " src1_sel:BYTE_0\n\t"
+
+#define ZRC4_E ZRC4_CORE(x0, x1, a0, a1, k0)   // even step: keystream -> k0
+#define ZRC4_O ZRC4_CORE(x1, x0, a1, a0, k1)   // odd step:  keystream -> k1
+#define ZRC4_W0(D)                                                                               \
+    ZRC4_E ZRC4_O ZRC4_XOR(D, BYTE_0, k0) ZRC4_E ZRC4_XOR(D, BYTE_1, k1)                        \
+    ZRC4_O ZRC4_XOR(D, BYTE_2, k0)
+#define ZRC4_W(DP, D)                                                                            \
+    ZRC4_E ZRC4_XOR(DP, BYTE_3, k1) ZRC4_O ZRC4_XOR(D, BYTE_0, k0)                              \
+    ZRC4_E ZRC4_XOR(D, BYTE_1, k1) ZRC4_O ZRC4_XOR(D, BYTE_2, k0)
+
+// 64 keystream bytes XORed into d[0..15] (little-endian dwords).
+__device__ __forceinline__ void xor64_asm(Rc4Lane &st, uint32_t (&d)[16])
+{
+    uint32_t b, k0, k1, a1;
+    asm volatile(
+        ZRC4_W0(d0) ZRC4_W(d0, d1) ZRC4_W(d1, d2) ZRC4_W(d2, d3)
+        ZRC4_W(d3, d4) ZRC4_W(d4, d5) ZRC4_W(d5, d6) ZRC4_W(d6, d7)
+        ZRC4_W(d7, d8) ZRC4_W(d8, d9) ZRC4_W(d9, d10) ZRC4_W(d10, d11)
+        ZRC4_W(d11, d12) ZRC4_W(d12, d13) ZRC4_W(d13, d14) ZRC4_W(d14, d15)
+        "s_waitcnt lgkmcnt(0)\n\t"
+        ZRC4_XOR(d15, BYTE_3, k1)
+        : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1),
+          [a0] "+v"(st.a0), [a1] "=&v"(a1), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
+          [d0] "+v"(d[0]), [d1] "+v"(d[1]), [d2] "+v"(d[2]), [d3] "+v"(d[3]),
+          [d4] "+v"(d[4]), [d5] "+v"(d[5]), [d6] "+v"(d[6]), [d7] "+v"(d[7]),
+          [d8] "+v"(d[8]), [d9] "+v"(d[9]), [d10] "+v"(d[10]), [d11] "+v"(d[11]),
+          [d12] "+v"(d[12]), [d13] "+v"(d[13]), [d14] "+v"(d[14]), [d15] "+v"(d[15])
+        :
+        : "memory");
+}
+
+__device__ __forceinline__ void load64(uint32_t (&d)[16], const uint4 *p)
+{
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4 v = p[q];
+        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void store64(uint4 *p, const uint32_t (&d)[16])
+{
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        p[q] = make_uint4(d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]);
+}
+
 // Crypt one lane's message in place: unaligned head bytes, 64-byte blocks
-// with the next block's loads issued before the current block's keystream,
-// 16-byte chunks, tail bytes.
+// (hand-written step; the next block's loads are issued before the current
+// block's keystream), 16-byte chunks, tail bytes.
 __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st,
                                               uint8_t *msg, uint32_t len)
 {
@@ -136,20 +214,28 @@ __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st,
     len -= head;
 
     uint4 *p = reinterpret_cast<uint4 *>(msg);
-    uint32_t nblk = len >> 6;
+    const uint32_t nblk = len >> 6;
     if (nblk) {
-        uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
-        for (uint32_t b = 0; b < nblk; ++b) {
-            uint4 n0, n1, n2, n3;
-            const bool more = (b + 1) < nblk;
-            if (more) { n0 = p[4]; n1 = p[5]; n2 = p[6]; n3 = p[7]; }
-            p[0] = xor16(S, st, c0);
-            p[1] = xor16(S, st, c1);
-            p[2] = xor16(S, st, c2);
-            p[3] = xor16(S, st, c3);
+        // Ping-pong buffers A/B, no loop-carried copies, and the next block's
+        // four loads issued unconditionally (re-reading the current block when
+        // there is none) so the compiler's vmcnt waits stay counted and never
+        // drain the prefetch.
+        uint32_t A[16], B[16];
+        load64(A, p);
+        uint32_t i = 0;
+        while (true) {
+            load64(B, (i + 1 < nblk) ? p + 4 : p);
+            xor64_asm(st, A);
+            store64(p, A);
+            if (++i == nblk) break;
             p += 4;
-            if (more) { c0 = n0; c1 = n1; c2 = n2; c3 = n3; }
+            load64(A, (i + 1 < nblk) ? p + 4 : p);
+            xor64_asm(st, B);
+            store64(p, B);
+            if (++i == nblk) break;
+            p += 4;
         }
+        p += 4;
     }
     uint32_t rem = len & 63u;
     while (rem >= 16u) {
@@ -212,11 +298,13 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         const uint32_t x = sxy & 255u, y = sxy >> 8;
         Rc4Lane st;
         st.col = col;
-        st.xa = (x << 8) | col;
+        st.x0 = (((x + 1u) & 255u) << 8) | col;
+        st.a0 = S[st.x0];
         st.ya = (y << 8) | col;
-        st.an = S[(((x + 1u) & 255u) << 8) | col];
+        st.ta = col;
+        st.x1 = col;
         crypt_message(S, st, payload + off[e], mylen);
-        xy[slot] = (uint16_t)((st.xa >> 8) | (st.ya & 0xFF00u));
+        xy[slot] = (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
     }
 
     if (whole) {
