@@ -97,21 +97,20 @@ class GpuRunner:
         self.payload = T(payload)
         self.off = T((np.arange(n, dtype=np.int64) * L))
         self.len = T(np.full(n, L, dtype=np.int32))
-        self.ids = T(np.arange(n, dtype=np.int32))
         self.ctx.sync(self.stream)
-        # cached raw arguments per batch: zrc4_crypt(ctx, ids, payload, off, len, n, stream)
+        # batch b = slots [b*S, (b+1)*S): zrc4_crypt_range(ctx, first_slot, payload, off, len, n, stream)
         lib, h, st = self.ctx._lib, self.ctx._h, C.c_void_p(self.stream.cuda_stream)
-        self._fn = lib.zrc4_crypt
+        self._fn = lib.zrc4_crypt_range
         self._args = []
         for b in range(R):
-            self._args.append((h, C.c_void_p(self.ids.data_ptr() + 4 * b * S), C.c_void_p(self.payload.data_ptr()),
+            self._args.append((h, b * S, C.c_void_p(self.payload.data_ptr()),
                                C.c_void_p(self.off.data_ptr() + 8 * b * S), C.c_void_p(self.len.data_ptr() + 4 * b * S),
                                S, st))
 
     def step(self, i: int) -> None:
         rc = self._fn(*self._args[i % self.R])
         if rc:
-            raise RuntimeError(f"zrc4_crypt failed: {rc}")
+            raise RuntimeError(f"zrc4_crypt_range failed: {rc}")
 
     def sync(self) -> None:
         self.torch.cuda.synchronize()

@@ -85,6 +85,18 @@ int zrc4_crypt(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payload,
                const uint64_t *off, const uint32_t *len, uint32_t n,
                void *stream);
 
+/* Contiguous-slot variants: entry i uses slot first_slot + i (no ids array).
+ * When first_slot is a multiple of 256 every workgroup owns a whole slot
+ * group and moves its state as one coalesced 64 KiB image: the fast path for
+ * a session engine that allocates its streams in groups.  Requires
+ * first_slot + n <= capacity.  Device pointers; asynchronous. */
+int zrc4_ksa_range(zrc4_ctx *ctx, uint32_t first_slot, const uint8_t *keys,
+                   const uint64_t *key_off, const uint32_t *key_len, uint32_t n,
+                   void *stream);
+int zrc4_crypt_range(zrc4_ctx *ctx, uint32_t first_slot, uint8_t *payload,
+                     const uint64_t *off, const uint32_t *len, uint32_t n,
+                     void *stream);
+
 /* Host-pointer variants: copy to the device (pinned staging), run, copy back,
  * block until done.  payload_bytes bounds the host payload buffer. */
 int zrc4_ksa_host(zrc4_ctx *ctx, const uint32_t *ids, const uint8_t *keys,

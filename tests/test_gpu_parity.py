@@ -132,6 +132,36 @@ def test_batch_whole_group_ids(ctx, batch_small):
     assert np.array_equal(pay, want)
 
 
+@pytest.mark.parametrize("first_slot", [512, 300])
+def test_crypt_range(ctx, torch_cuda, first_slot):
+    """Contiguous-slot entry: aligned first_slot (whole-group image path) and
+    unaligned first_slot (per-lane gather path), ragged lengths."""
+    torch = torch_cuda
+    rng = np.random.default_rng(first_slot)
+    n = 600
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(n)]
+    kblob = torch.from_numpy(np.frombuffer(b"".join(keys), dtype=np.uint8).copy()).cuda()
+    koff = torch.arange(n, dtype=torch.int64, device="cuda") * 16
+    klen = torch.full((n,), 16, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    ctx.ksa_range(first_slot, klen, koff, kblob, stream=s)
+    L = rng.integers(0, 1500, n).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(L[:-1])]).astype(np.uint64)
+    data = rng.integers(0, 256, int(L.sum()) + 1, dtype=np.uint8)
+    want = data.copy()
+    for i in range(n):
+        a, z = int(off[i]), int(off[i] + L[i])
+        want[a:z] = np.frombuffer(pyoracle.Rc4(keys[i]).encryption(want[a:z].tobytes()), np.uint8)
+    pay = torch.from_numpy(data).cuda()
+    ctx.crypt_range(first_slot, pay, torch.from_numpy(off.view(np.int64)).cuda(),
+                    torch.from_numpy(L.view(np.int32)).cuda(), stream=s)
+    ctx.sync(s)
+    assert np.array_equal(pay.cpu().numpy(), want)
+    with pytest.raises(ZRC4Error):
+        ctx.crypt_range(ctx.capacity - 10, pay, torch.from_numpy(off.view(np.int64)).cuda(),
+                        torch.from_numpy(L.view(np.int32)).cuda(), stream=s)
+
+
 def test_split_invariance_batched(ctx):
     """N calls of a few bytes == one call of the sum (keystream continues)."""
     rng = np.random.default_rng(4)

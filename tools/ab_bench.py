@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""A/B timing of libzrc4 variants inside ONE process on ONE GPU.
+
+Cross-box numbers for LDS-bound loops move by up to ~12 % between MI355X
+devices (MI355X_MICROARCH.md, DVFS give-back item 5), so kernel changes are
+judged here: every variant library (built with -D switches by
+zsummerx_amd.build.build_variant) gets its own context seeded identically;
+outputs of one batch are compared byte-for-byte across variants (they must be
+identical); then timed rounds are interleaved and the median per-launch time
+(HIP events on the launch stream) is reported per variant.
+
+  python tools/ab_bench.py --variant base: --variant o1:ZRC4_STEP_ORDER=1 \
+      --workloads cfg2,cfg3,cfg5 --rounds 7 --launches 20
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import statistics
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+SHAPES = {"cfg2": (4096, 1024), "cfg3": (65536, 256), "cfg4": (1024, 65536), "cfg5": (524288, 1024)}
+
+
+def parse_variant(v: str):
+    name, _, defs = v.partition(":")
+    d = {}
+    for kv in filter(None, defs.split(",")):
+        k, _, val = kv.partition("=")
+        d[k] = val or "1"
+    return name, d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", action="append", required=True, help="name:DEF=v,DEF2=v")
+    ap.add_argument("--workloads", default="cfg2,cfg3,cfg5")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--footprint-mib", type=int, default=640)
+    ap.add_argument("--build-only", action="store_true")
+    args = ap.parse_args()
+
+    from zsummerx_amd import build
+    variants = []
+    for v in args.variant:
+        name, defs = parse_variant(v)
+        variants.append((name, build.build_variant(name, defs)))
+    if args.build_only:
+        print("built", [str(p) for _, p in variants])
+        return
+
+    import torch  # one HIP runtime for every variant library (see _capi.load)
+    from zsummerx_amd import _capi, synth
+
+    libs = [(n, _capi.load(p)) for n, p in variants]
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    st = C.c_void_p(stream.cuda_stream)
+    report = {}
+    for wl in args.workloads.split(","):
+        if wl in SHAPES:
+            S, L = SHAPES[wl]
+        else:                                   # custom "SxL"
+            S, L = (int(v) for v in wl.lower().split("x"))
+        R = max(1, -(-args.footprint_mib * (1 << 20) // (S * (L + 256))))
+        R = min(R, (1 << 24) // S)
+        n = S * R
+        keys = torch.from_numpy(synth.keys(0, n).reshape(-1)).to(dev)
+        adv = torch.from_numpy(synth.advance(0, n).view(np.int32)).to(dev)
+        klen = torch.full((n,), 16, dtype=torch.int32, device=dev)
+        koff = torch.arange(n, dtype=torch.int64, device=dev) * 16
+        pay = torch.from_numpy(synth.payload(0, n * L, threads=8)).to(dev)
+        off = torch.arange(n, dtype=torch.int64, device=dev) * L
+        ln = torch.full((n,), L, dtype=torch.int32, device=dev)
+        scratch = torch.zeros(1000, dtype=torch.uint8, device=dev)
+        zoff = torch.zeros(n, dtype=torch.int64, device=dev)
+        ctxs = []
+        for name, lib in libs:
+            h = C.c_void_p()
+            _capi.check(lib.zrc4_create(C.byref(h), 0, n), f"{name} create")
+            _capi.check(lib.zrc4_ksa_range(h, 0, C.c_void_p(keys.data_ptr()), C.c_void_p(koff.data_ptr()),
+                                           C.c_void_p(klen.data_ptr()), n, st))
+            _capi.check(lib.zrc4_crypt(h, None, C.c_void_p(scratch.data_ptr()), C.c_void_p(zoff.data_ptr()),
+                                       C.c_void_p(adv.data_ptr()), n, st))
+            ctxs.append(h)
+        torch.cuda.synchronize()
+        # identical-output check on batch 0
+        ref = None
+        for (name, lib), h in zip(libs, ctxs):
+            buf = pay[: S * L].clone()
+            _capi.check(lib.zrc4_crypt_range(h, 0, C.c_void_p(buf.data_ptr()), C.c_void_p(off.data_ptr()),
+                                             C.c_void_p(ln.data_ptr()), S, st))
+            _capi.check(lib.zrc4_sync(h, st))
+            if ref is None:
+                ref = buf
+            elif not torch.equal(ref, buf):
+                raise SystemExit(f"variant {name} output differs from {libs[0][0]} on {wl}")
+        times = {name: [] for name, _ in libs}
+        step = 1
+        for r in range(args.rounds):
+            for (name, lib), h in zip(libs, ctxs):
+                evs = []
+                for i in range(args.launches):
+                    b = step % R
+                    step += 1
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    rc = lib.zrc4_crypt_range(h, b * S, C.c_void_p(pay.data_ptr()),
+                                              C.c_void_p(off.data_ptr() + 8 * b * S),
+                                              C.c_void_p(ln.data_ptr() + 4 * b * S), S, st)
+                    e1.record(stream)
+                    evs.append((e0, e1))
+                    if rc:
+                        raise SystemExit(f"{name}: crypt failed {rc}")
+                torch.cuda.synchronize()
+                times[name].extend(a.elapsed_time(b_) * 1e3 for a, b_ in evs)
+        B = 2 * S * L + 516 * S
+        report[wl] = {name: {"median_us": round(statistics.median(t), 2), "min_us": round(min(t), 2),
+                             "hbm_frac": round(B / (statistics.median(t) * 1e-6) / 8e12, 4)}
+                      for name, t in times.items()}
+        print(wl, json.dumps(report[wl]), flush=True)
+        for (name, lib), h in zip(libs, ctxs):
+            lib.zrc4_destroy(h)
+        del keys, adv, pay, off, ln, klen, koff, zoff
+        torch.cuda.empty_cache()
+    print(json.dumps(report))
+
+
+if __name__ == "__main__":
+    main()

@@ -88,6 +88,16 @@ class Context:
         check(self._lib.zrc4_crypt(self._h, _ptr(ids), _ptr(payload), _ptr(off), _ptr(length),
                                    n, _stream(stream)), "zrc4_crypt")
 
+    def ksa_range(self, first_slot: int, key_len, key_off, keys, n=None, stream=None) -> None:
+        n = int(key_len.numel() if n is None else n)
+        check(self._lib.zrc4_ksa_range(self._h, int(first_slot), _ptr(keys), _ptr(key_off),
+                                       _ptr(key_len), n, _stream(stream)), "zrc4_ksa_range")
+
+    def crypt_range(self, first_slot: int, payload, off, length, n=None, stream=None) -> None:
+        n = int(length.numel() if n is None else n)
+        check(self._lib.zrc4_crypt_range(self._h, int(first_slot), _ptr(payload), _ptr(off),
+                                         _ptr(length), n, _stream(stream)), "zrc4_crypt_range")
+
     def sync(self, stream=None) -> None:
         check(self._lib.zrc4_sync(self._h, _stream(stream)), "zrc4_sync")
 

@@ -30,6 +30,8 @@ SIGNATURES = [
     ("zrc4_capacity", C.c_uint32, [_P]),
     ("zrc4_ksa", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_crypt", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
+    ("zrc4_ksa_range", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P]),
+    ("zrc4_crypt_range", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_ksa_host", C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, C.c_uint32]),
     ("zrc4_crypt_host", C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, C.c_uint32]),
     ("zrc4_make_sbox", C.c_int, [_P, C.c_uint32, _P, C.c_size_t]),

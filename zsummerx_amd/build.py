@@ -49,6 +49,19 @@ def build_lib(force: bool = False, extra_flags=()) -> Path:
     return LIB
 
 
+def build_variant(name: str, defines: dict) -> Path:
+    """A/B builds: the same library under another name with -D switches
+    (tools/ab_bench.py loads several side by side in one process)."""
+    out = PKG / f"libzrc4_{name}.so"
+    if _stale(out, HIP_DEPS):
+        BUILD.mkdir(exist_ok=True)
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               f"-I{ROOT / 'include'}", *[f"-D{k}={v}" for k, v in defines.items()],
+               "-o", str(out), *map(str, HIP_SOURCES)]
+        subprocess.run(cmd, check=True, cwd=BUILD)
+    return out
+
+
 def build_synth(force: bool = False) -> Path:
     src = CSRC / "synth.cpp"
     if force or _stale(SYNTH, [src]):

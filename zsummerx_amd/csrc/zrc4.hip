@@ -59,25 +59,25 @@ int grow_stage(zrc4_ctx *c, size_t bytes)
 
 size_t align16(size_t v) { return (v + 15u) & ~(size_t)15u; }
 
-int launch_crypt(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_t *off,
-                 const uint32_t *len, uint32_t n, hipStream_t s)
+int launch_crypt(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, uint8_t *payload,
+                 const uint64_t *off, const uint32_t *len, uint32_t n, hipStream_t s)
 {
     if (n == 0) return ZRC4_OK;
-    if (!ids && n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    if (!ids && (uint64_t)first_slot + n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
     const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
     hipLaunchKernelGGL(zrc4::crypt_kernel, dim3(grid), dim3(zrc4::kGroup), 0, s, c->arena,
-                       c->xy, ids, payload, off, len, n, c->capacity, c->err);
+                       c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err);
     return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
 }
 
-int launch_ksa(zrc4_ctx *c, const uint32_t *ids, const uint8_t *keys, const uint64_t *key_off,
-               const uint32_t *key_len, uint32_t n, hipStream_t s)
+int launch_ksa(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, const uint8_t *keys,
+               const uint64_t *key_off, const uint32_t *key_len, uint32_t n, hipStream_t s)
 {
     if (n == 0) return ZRC4_OK;
-    if (!ids && n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    if (!ids && (uint64_t)first_slot + n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
     const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
     hipLaunchKernelGGL(zrc4::ksa_kernel, dim3(grid), dim3(zrc4::kGroup), 0, s, c->arena, c->xy,
-                       ids, keys, key_off, key_len, n, c->capacity, c->err);
+                       ids, first_slot, keys, key_off, key_len, n, c->capacity, c->err);
     return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
 }
 
@@ -161,7 +161,7 @@ int zrc4_ksa(zrc4_ctx *c, const uint32_t *ids, const uint8_t *keys, const uint64
     if (n && (!key_len || !key_off)) return ZRC4_ERR_INVALID_ARG;
     int rc = set_device(c);
     if (rc) return rc;
-    return launch_ksa(c, ids, keys, key_off, key_len, n, (hipStream_t)stream);
+    return launch_ksa(c, ids, 0, keys, key_off, key_len, n, (hipStream_t)stream);
 }
 
 int zrc4_crypt(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_t *off,
@@ -171,7 +171,27 @@ int zrc4_crypt(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_
     if (n && (!payload || !off || !len)) return ZRC4_ERR_INVALID_ARG;
     int rc = set_device(c);
     if (rc) return rc;
-    return launch_crypt(c, ids, payload, off, len, n, (hipStream_t)stream);
+    return launch_crypt(c, ids, 0, payload, off, len, n, (hipStream_t)stream);
+}
+
+int zrc4_ksa_range(zrc4_ctx *c, uint32_t first_slot, const uint8_t *keys,
+                   const uint64_t *key_off, const uint32_t *key_len, uint32_t n, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n && (!key_len || !key_off)) return ZRC4_ERR_INVALID_ARG;
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_ksa(c, nullptr, first_slot, keys, key_off, key_len, n, (hipStream_t)stream);
+}
+
+int zrc4_crypt_range(zrc4_ctx *c, uint32_t first_slot, uint8_t *payload, const uint64_t *off,
+                     const uint32_t *len, uint32_t n, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n && (!payload || !off || !len)) return ZRC4_ERR_INVALID_ARG;
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_crypt(c, nullptr, first_slot, payload, off, len, n, (hipStream_t)stream);
 }
 
 int zrc4_sync(zrc4_ctx *c, void *stream)
@@ -204,7 +224,7 @@ int zrc4_ksa_host(zrc4_ctx *c, const uint32_t *ids, const uint8_t *keys, size_t 
     memcpy(c->h_stage + o_len, key_len, (size_t)n * 4);
     if (keys_bytes) memcpy(c->h_stage + o_key, keys, keys_bytes);
     ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
-    rc = launch_ksa(c, ids ? (const uint32_t *)(c->d_stage + o_ids) : nullptr,
+    rc = launch_ksa(c, ids ? (const uint32_t *)(c->d_stage + o_ids) : nullptr, 0,
                     c->d_stage + o_key, (const uint64_t *)(c->d_stage + o_off),
                     (const uint32_t *)(c->d_stage + o_len), n, c->stream);
     if (rc) return rc;
@@ -232,7 +252,7 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
     memcpy(c->h_stage + o_len, len, (size_t)n * 4);
     if (payload_bytes) memcpy(c->h_stage + o_pay, payload, payload_bytes);
     ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
-    rc = launch_crypt(c, ids ? (const uint32_t *)(c->d_stage + o_ids) : nullptr,
+    rc = launch_crypt(c, ids ? (const uint32_t *)(c->d_stage + o_ids) : nullptr, 0,
                       c->d_stage + o_pay, (const uint64_t *)(c->d_stage + o_off),
                       (const uint32_t *)(c->d_stage + o_len), n, c->stream);
     if (rc) return rc;

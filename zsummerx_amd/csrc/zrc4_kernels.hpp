@@ -136,6 +136,31 @@ __device__ __forceinline__ uint4 xor16(uint8_t *S, Rc4Lane &st, uint4 v)
 // is retired by step s+1's waits) with one SDWA xor on that byte lane.
 // (ds_read_u8_d16_hi does NOT preserve the low half on gfx950 -- measured --
 // so keystream bytes are not packed through d16 loads.)
+//
+// Registers: XC = address of S[x] for this step, XN = address of S[x+1]
+// (computed one step ahead, so only  y+=a -> read b -> write a -> read S[x+1]
+// sit between S[x+1] arriving and the next S[x+1] read being issued).  XC is
+// free after the S[x] = b write and becomes x+2 (the next step's XN).
+// Per byte: 4 VALU + 5 LDS + 2 waits.
+#ifndef ZRC4_STEP_ORDER
+#define ZRC4_STEP_ORDER 1
+#endif
+#if ZRC4_STEP_ORDER == 2
+#define ZRC4_CORE(XC, XN, A, P, K)                                                               \
+    "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
+    "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
+    "ds_read_u8 %[b], %[ya]\n\t"                                                                 \
+    "ds_write_b8 %[ya], %[" #A "]\n\t"                                                           \
+    "ds_read_u8 %[" #P "], %[" #XN "]\n\t"                                                       \
+    "s_waitcnt lgkmcnt(2)\n\t"                                                                   \
+    "ds_write_b8 %[" #XC "], %[b]\n\t"                                                           \
+    "v_add_u32_sdwa %[ta], %[" #A "], %[b] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "           \
+    "src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"                                                        \
+    "ds_read_u8 %[" #K "], %[ta]\n\t"                                                            \
+    "v_add_u32_sdwa %[" #XC "], 1, %[" #XN "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "        \
+    "src0_sel:DWORD src1_sel:BYTE_1\n\t"                                                         \
+    "s_waitcnt lgkmcnt(2)\n\t"
+#else  // order 1: x+1 computed inside the step (XN derived from XC before the read)
 #define ZRC4_CORE(XC, XN, A, P, K)                                                               \
     "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
     "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
@@ -150,6 +175,14 @@ __device__ __forceinline__ uint4 xor16(uint8_t *S, Rc4Lane &st, uint4 v)
     "src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"                                                        \
     "ds_read_u8 %[" #K "], %[ta]\n\t"                                                            \
     "s_waitcnt lgkmcnt(2)\n\t"
+#endif
+#if ZRC4_STEP_ORDER == 2
+#define ZRC4_X1_INIT                                                                             \
+    "v_add_u32_sdwa %[x1], 1, %[x0] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "                  \
+    "src0_sel:DWORD src1_sel:BYTE_1\n\t"
+#else
+#define ZRC4_X1_INIT ""
+#endif
 
 #define ZRC4_XOR(D, SEL, K)                                                                      \
     "v_xor_b32_sdwa %[" #D "], %[" #D "], %[" #K "] dst_sel:" #SEL                               \
@@ -164,11 +197,14 @@ __device__ __forceinline__ uint4 xor16(uint8_t *S, Rc4Lane &st, uint4 v)
     ZRC4_E ZRC4_XOR(DP, BYTE_3, k1) ZRC4_O ZRC4_XOR(D, BYTE_0, k0)                              \
     ZRC4_E ZRC4_XOR(D, BYTE_1, k1) ZRC4_O ZRC4_XOR(D, BYTE_2, k0)
 
-// 64 keystream bytes XORed into d[0..15] (little-endian dwords).
-__device__ __forceinline__ void xor64_asm(Rc4Lane &st, uint32_t (&d)[16])
+// 64 keystream bytes XORed into d[0..15] (little-endian dwords).  On entry
+// st.x0 / st.a0 / st.ya hold the C-step state; x1 (byte 0 = col) is derived
+// here.  On exit every asm output has landed (final lgkmcnt(0)).
+__device__ __forceinline__ void xor64_asm(Rc4Lane &st, uint4 (&q)[4])
 {
     uint32_t b, k0, k1, a1;
     asm volatile(
+        ZRC4_X1_INIT
         ZRC4_W0(d0) ZRC4_W(d0, d1) ZRC4_W(d1, d2) ZRC4_W(d2, d3)
         ZRC4_W(d3, d4) ZRC4_W(d4, d5) ZRC4_W(d5, d6) ZRC4_W(d6, d7)
         ZRC4_W(d7, d8) ZRC4_W(d8, d9) ZRC4_W(d9, d10) ZRC4_W(d10, d11)
@@ -177,38 +213,44 @@ __device__ __forceinline__ void xor64_asm(Rc4Lane &st, uint32_t (&d)[16])
         ZRC4_XOR(d15, BYTE_3, k1)
         : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1),
           [a0] "+v"(st.a0), [a1] "=&v"(a1), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
-          [d0] "+v"(d[0]), [d1] "+v"(d[1]), [d2] "+v"(d[2]), [d3] "+v"(d[3]),
-          [d4] "+v"(d[4]), [d5] "+v"(d[5]), [d6] "+v"(d[6]), [d7] "+v"(d[7]),
-          [d8] "+v"(d[8]), [d9] "+v"(d[9]), [d10] "+v"(d[10]), [d11] "+v"(d[11]),
-          [d12] "+v"(d[12]), [d13] "+v"(d[13]), [d14] "+v"(d[14]), [d15] "+v"(d[15])
+          [d0] "+v"(q[0].x), [d1] "+v"(q[0].y), [d2] "+v"(q[0].z), [d3] "+v"(q[0].w),
+          [d4] "+v"(q[1].x), [d5] "+v"(q[1].y), [d6] "+v"(q[1].z), [d7] "+v"(q[1].w),
+          [d8] "+v"(q[2].x), [d9] "+v"(q[2].y), [d10] "+v"(q[2].z), [d11] "+v"(q[2].w),
+          [d12] "+v"(q[3].x), [d13] "+v"(q[3].y), [d14] "+v"(q[3].z), [d15] "+v"(q[3].w)
         :
         : "memory");
 }
 
-__device__ __forceinline__ void load64(uint32_t (&d)[16], const uint4 *p)
+// 64-byte blocks are kept as uint4[4] so every 16 bytes sits in an aligned
+// 4-register tuple (one dwordx4 each); as uint32_t[16] the register allocator
+// placed them off-tuple and hipcc split the loads into dwordx2/dwordx4 pieces.
+__device__ __forceinline__ void load64(uint4 (&q)[4], const uint4 *p)
 {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint4 v = p[q];
-        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
-    }
+    for (int i = 0; i < 4; ++i) q[i] = p[i];
 }
 
-__device__ __forceinline__ void store64(uint4 *p, const uint32_t (&d)[16])
+__device__ __forceinline__ void store64(uint4 *p, const uint4 (&q)[4])
 {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-        p[q] = make_uint4(d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]);
+    for (int i = 0; i < 4; ++i) p[i] = q[i];
+}
+
+// Bytes before the first 16-byte boundary of a message (<= len).
+__device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
+{
+    const uint32_t h = (16u - ((uint32_t)(uintptr_t)msg & 15u)) & 15u;
+    return h < len ? h : len;
 }
 
 // Crypt one lane's message in place: unaligned head bytes, 64-byte blocks
 // (hand-written step; the next block's loads are issued before the current
-// block's keystream), 16-byte chunks, tail bytes.
-__device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st,
-                                              uint8_t *msg, uint32_t len)
+// block's keystream), 16-byte chunks, tail bytes.  If `pre` is set, A already
+// holds the first 64-byte block (loaded by the caller ahead of the LDS fill).
+__device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st, uint8_t *msg,
+                                              uint32_t len, uint4 (&A)[4], bool pre)
 {
-    uint32_t head = (16u - ((uint32_t)(uintptr_t)msg & 15u)) & 15u;
-    if (head > len) head = len;
+    const uint32_t head = head_bytes(msg, len);
     for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
     msg += head;
     len -= head;
@@ -220,8 +262,8 @@ __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st,
         // four loads issued unconditionally (re-reading the current block when
         // there is none) so the compiler's vmcnt waits stay counted and never
         // drain the prefetch.
-        uint32_t A[16], B[16];
-        load64(A, p);
+        uint4 B[4];
+        if (!pre) load64(A, p);
         uint32_t i = 0;
         while (true) {
             load64(B, (i + 1 < nblk) ? p + 4 : p);
@@ -247,54 +289,75 @@ __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st,
     for (uint32_t i = 0; i < rem; ++i) t[i] ^= (uint8_t)prga_step(S, st);
 }
 
+// Which slot batch entry e maps to, and whether workgroup w owns one whole
+// aligned 256-slot group g (then state moves as a coalesced 64 KiB image).
+//   ids == NULL : slot = first_slot + e; whole iff first_slot % 256 == 0
+//                 (entries >= n of the last group belong to no other
+//                 workgroup; their state is copied back unchanged)
+//   ids != NULL : whole iff the 256 ids are exactly g*256 .. g*256+255
+#define ZRC4_INVALID 0xFFFFFFFFu
+
 // ---------------------------------------------------------------------------
 // crypt_kernel: batched RC4Encryption::encryption.
 // grid = ceil(n / 256) workgroups of 256 threads; workgroup w handles batch
-// entries [w*256, w*256+256).
+// entries [w*256, w*256+256).  The prologue issues every independent load
+// first (group image, len/off/xy, the first payload block) so it costs about
+// two HBM round trips instead of a dependent chain of them.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256, 2)
 crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
-             const uint32_t *__restrict__ ids, uint8_t *__restrict__ payload,
-             const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
-             uint32_t n, uint32_t capacity, uint32_t *__restrict__ err)
+             const uint32_t *__restrict__ ids, uint32_t first_slot,
+             uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
+             const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
+             uint32_t *__restrict__ err)
 {
     __shared__ __attribute__((aligned(16))) uint8_t S[kGroupBytes];
 
     const uint32_t j = threadIdx.x;
     const uint32_t e = blockIdx.x * kGroup + j;
     const bool valid = e < n;
-    uint32_t slot = valid ? (ids ? ids[e] : e) : 0xFFFFFFFFu;
+    const uint32_t mylen0 = valid ? len[e] : 0u;
+    const uint64_t myoff = valid ? off[e] : 0u;
+    uint32_t slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
     if (valid && slot >= capacity) {
         atomicOr(err, kErrSlotRange);
-        slot = 0xFFFFFFFFu;
+        slot = ZRC4_INVALID;
     }
-    const bool active = slot != 0xFFFFFFFFu;
-    const uint32_t mylen = active ? len[e] : 0u;
+    const bool active = slot != ZRC4_INVALID;
+    const uint32_t mylen = active ? mylen0 : 0u;
+    const uint16_t sxy = (active && mylen) ? xy[slot] : (uint16_t)0;
 
-    // Fast path: this workgroup covers one whole aligned group.  With
-    // ids == NULL group w is exactly slots [w*256, w*256+256) (entries >= n
-    // belong to no other workgroup, and their state is copied back unchanged).
     bool whole;
     uint32_t g;
     if (!ids) {
-        whole = true;
-        g = blockIdx.x;
+        whole = (first_slot & 255u) == 0u;
+        g = (first_slot >> 8) + blockIdx.x;
     } else {
-        const uint32_t first = (blockIdx.x * kGroup < n) ? ids[blockIdx.x * kGroup] : 0u;
+        const uint32_t first = ids[blockIdx.x * kGroup];
         g = first >> 8;
         whole = __syncthreads_and(active && slot == ((first & ~255u) + j) && (first & 255u) == 0u);
     }
 
     const uint32_t col = col_of(j);
+    uint8_t *msg = payload + myoff;
+    uint4 A[4];
+    const bool pre = active && mylen >= 64u && head_bytes(msg, mylen) == 0u;
     if (whole) {
-        image_to_lds(S, arena + (size_t)g * kGroupBytes);
+        uint4 img[16];
+        const uint4 *src = reinterpret_cast<const uint4 *>(arena + (size_t)g * kGroupBytes);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) img[i] = src[i * 256 + j];
+        if (pre) load64(A, reinterpret_cast<const uint4 *>(msg));
+        uint4 *dst = reinterpret_cast<uint4 *>(S);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dst[i * 256 + j] = img[i];
         __syncthreads();
-    } else if (active && mylen) {
-        gather_column(S, col, arena, slot);
+    } else {
+        if (pre) load64(A, reinterpret_cast<const uint4 *>(msg));
+        if (active && mylen) gather_column(S, col, arena, slot);
     }
 
     if (active && mylen) {
-        const uint16_t sxy = xy[slot];
         const uint32_t x = sxy & 255u, y = sxy >> 8;
         Rc4Lane st;
         st.col = col;
@@ -303,7 +366,7 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         st.ya = (y << 8) | col;
         st.ta = col;
         st.x1 = col;
-        crypt_message(S, st, payload + off[e], mylen);
+        crypt_message(S, st, msg, mylen, A, pre);
         xy[slot] = (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
     }
 
@@ -320,7 +383,8 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256, 2)
 ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
-           const uint32_t *__restrict__ ids, const uint8_t *__restrict__ keys,
+           const uint32_t *__restrict__ ids, uint32_t first_slot,
+           const uint8_t *__restrict__ keys,
            const uint64_t *__restrict__ key_off, const uint32_t *__restrict__ key_len,
            uint32_t n, uint32_t capacity, uint32_t *__restrict__ err)
 {
@@ -329,26 +393,26 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     const uint32_t j = threadIdx.x;
     const uint32_t e = blockIdx.x * kGroup + j;
     const bool valid = e < n;
-    uint32_t slot = valid ? (ids ? ids[e] : e) : 0xFFFFFFFFu;
+    uint32_t slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
     if (valid && slot >= capacity) {
         atomicOr(err, kErrSlotRange);
-        slot = 0xFFFFFFFFu;
+        slot = ZRC4_INVALID;
     }
-    const bool active = slot != 0xFFFFFFFFu;
+    const bool active = slot != ZRC4_INVALID;
 
     bool whole;
     uint32_t g;
     if (!ids) {
         // Entries >= n of the last group are not re-seeded: load the image so
         // their state is written back unchanged.
-        whole = true;
-        g = blockIdx.x;
+        whole = (first_slot & 255u) == 0u;
+        g = (first_slot >> 8) + blockIdx.x;
     } else {
         const uint32_t first = (blockIdx.x * kGroup < n) ? ids[blockIdx.x * kGroup] : 0u;
         g = first >> 8;
         whole = __syncthreads_and(active && slot == ((first & ~255u) + j) && (first & 255u) == 0u);
     }
-    const bool partial = !ids && (blockIdx.x + 1u) * kGroup > n;
+    const bool partial = (blockIdx.x + 1u) * kGroup > n;
     const uint32_t col = col_of(j);
 
     if (whole && partial) {
