@@ -118,17 +118,41 @@ class GpuRunner:
     def check(self) -> None:
         self.ctx.sync(self.stream)
 
+    def timed_steps(self, first: int, k: int):
+        """Launch steps first..first+k-1; return each launch's duration (ms),
+        measured with HIP events on the launch stream."""
+        torch = self.torch
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(k)]
+        for i in range(k):
+            ev[i][0].record(self.stream)
+            self.step(first + i)
+            ev[i][1].record(self.stream)
+        self.sync()
+        return [a.elapsed_time(b) for a, b in ev]
 
-def run_gpu(args, ws, rank, local):
+
+def run_bench(args, ws, rank, local, backend="nccl", make_runner=None):
+    """Shared orchestration (GPU bench and the gloo CPU test): W untimed steps,
+    barrier + sync, K timed steps, sync + barrier, max over ranks.  Sessions
+    shard across ranks by global id (shard_first); no data-path collective."""
     import torch
     import torch.distributed as dist
 
+    on_gpu = backend == "nccl"
     if ws > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if on_gpu:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     S, L = CONFIG_SHAPES[args.workload]
     R = rotation_batches(S, L, args.footprint_mib) if args.footprint_mib > 0 else 1
-    runner = GpuRunner(torch, local, S, L, R, shard_first(rank, R, S))
+    if make_runner is None:
+        runner = GpuRunner(torch, local, S, L, R, shard_first(rank, R, S))
+    else:
+        runner = make_runner(S, L, R, shard_first(rank, R, S))
+    dev = "cuda" if on_gpu else "cpu"
 
     def barrier():
         if ws > 1:
@@ -138,43 +162,32 @@ def run_gpu(args, ws, rank, local):
         runner.step(i)
     runner.sync()
 
-    # kernel-duration probe: HIP events bracketing each launch on the launch stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
     barrier()
     runner.sync()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(runner.stream)
-        runner.step(args.warmup + i)
-        ev[i][1].record(runner.stream)
+    kern_ms = runner.timed_steps(args.warmup, args.steps)
     runner.sync()
     barrier()
     elapsed = time.perf_counter() - t0
     runner.check()
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed, statistics.mean(kern_ms)], dtype=torch.float64, device=dev)
     if ws > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    tmax = float(t.item())
-    k = torch.tensor([statistics.mean(kern_ms)], dtype=torch.float64, device="cuda")
-    if ws > 1:
-        dist.all_reduce(k, op=dist.ReduceOp.MAX)
-    kern_avg_ms = float(k.item())
+    tmax, kern_avg_ms = float(t[0].item()), float(t[1].item())
 
     res = None
     if rank == 0:
         total_payload = ws * args.steps * S * L
         res = build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload)
-        if args.cpu_seconds > 0 and ws == 1:
+        if args.cpu_seconds > 0 and ws == 1 and make_runner is None:
             res["cpu_baseline"] = cpu_baseline(args, S, L)
         else:
             res["cpu_baseline"] = None
     if ws > 1:
         dist.barrier()
         dist.destroy_process_group()
-    return res
+    return res, runner
 
 
 CONFIG_SHAPES = {"cfg2": (4096, 1024), "cfg3": (65536, 256), "cfg4": (1024, 65536),
@@ -284,6 +297,55 @@ def cpu_baseline(args, S, L):
                       f"~{budget:.0f}s total: median of >=5 runs of >=200 ms, 1 thread then {cores} threads"}
 
 
+# ------------------------------------------------------- host-inclusive rate
+def host_inclusive(args):
+    """The path starts in a socket recv buffer and ends in a send buffer, so
+    the rate including PCIe is measured too (reported in DESIGN.md, never as
+    `value`): pinned host payload, sessions split into --chunks chunks pipelined
+    over --streams HIP streams (H2D -> zrc4_crypt_range -> D2H per chunk), wall
+    clock from the first H2D to the last D2H, median of --steps passes."""
+    import torch
+    from zsummerx_amd import Context, synth
+    S, L = CONFIG_SHAPES[args.workload]
+    dev = torch.device("cuda", 0)
+    ctx = Context(0, S)
+    w = synth.make(0, S, L, threads=8)
+    T = lambda a: torch.from_numpy(a).to(dev)
+    ctx.ksa(T(w.key_len.view(np.int32)), T(w.key_off.view(np.int64)), T(w.keys))
+    ctx.crypt(torch.zeros(1000, dtype=torch.uint8, device=dev), torch.zeros(S, dtype=torch.int64, device=dev),
+              T(w.adv.view(np.int32)))
+    ctx.sync()
+    host = torch.from_numpy(w.payload).pin_memory()
+    devbuf = torch.empty(S * L, dtype=torch.uint8, device=dev)
+    off = T(w.off.view(np.int64))
+    ln = T(w.length.view(np.int32))
+    nchunk = max(1, min(args.chunks, S // 256))
+    per = -(-S // nchunk)
+    per = -(-per // 256) * 256                      # whole 256-slot groups per chunk
+    streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
+    times = []
+    for it in range(args.warmup + args.steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for c, s0 in enumerate(range(0, S, per)):
+            n = min(per, S - s0)
+            st = streams[c % len(streams)]
+            a, z = s0 * L, (s0 + n) * L
+            with torch.cuda.stream(st):
+                devbuf[a:z].copy_(host[a:z], non_blocking=True)
+                ctx.crypt_range(s0, devbuf, off[s0:], ln[s0:], n=n, stream=st)
+                host[a:z].copy_(devbuf[a:z], non_blocking=True)
+        torch.cuda.synchronize()
+        if it >= args.warmup:
+            times.append(time.perf_counter() - t0)
+    ctx.sync()
+    t = statistics.median(times)
+    return {"metric": "RC4 GiB/s host-inclusive (pinned H2D -> kernel -> D2H)",
+            "value": round(S * L / t / GIB, 3), "unit": "GiB/s", "ms_per_pass": round(t * 1e3, 4),
+            "workload": args.workload, "chunks": nchunk, "streams": len(streams),
+            "pcie_bytes_per_pass": 2 * S * L, "note": "not the headline value (DESIGN.md)"}
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     p.add_argument("--gpus", type=int, default=1)
@@ -295,15 +357,22 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="CPU baseline time budget on rank 0 at N=1 (0 disables)")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--host-inclusive", action="store_true",
+                   help="measure the PCIe-inclusive rate instead (DESIGN.md), one JSON line")
+    p.add_argument("--chunks", type=int, default=8)
+    p.add_argument("--streams", type=int, default=3)
     return p.parse_args(argv)
 
 
 def main(argv=None):
     args = parse(argv)
     ws, rank, local = dist_env()
+    if args.host_inclusive:
+        print(json.dumps(host_inclusive(args)), flush=True)
+        return
     if ws != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE")
-    res = run_gpu(args, ws, rank, local)
+    res, _ = run_bench(args, ws, rank, local)
     if rank == 0:
         print(json.dumps(res), flush=True)
 

@@ -1,0 +1,118 @@
+"""CPU multi-rank tests (gloo, world_size 2) of bench.py's distributed path.
+
+The GPU bench shards sessions across ranks by global id with no data-path
+collective; torch.distributed carries only the start/stop
+barrier and the max-over-ranks time.  Here the same orchestration
+(bench.run_bench) runs on two CPU processes with a test-side runner that
+crypts its shard with the oracle, and we check: disjoint, complete shards;
+each rank's ciphertext equals the single-process result for those global
+sessions; rank 0 reports the whole-job aggregate from the MAX rank time.
+"""
+import hashlib
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+sys.path.insert(0, str(ROOT))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class OracleRunner:
+    """Runner with the GpuRunner interface, backed by the CPU oracle."""
+
+    def __init__(self, S, L, R, first):
+        import pyoracle
+        from zsummerx_amd import synth
+        self.S, self.L, self.R, self.first = S, L, R, first
+        w = synth.make(first, S * R, L)
+        self.w = w
+        self.ob = pyoracle.Batch(S * R)
+        self.ob.make_sbox(w.keys, w.key_off, w.key_len)
+        self.ob.crypt(np.zeros(1000, dtype=np.uint8), np.zeros(S * R, dtype=np.uint64), w.adv)
+        self.steps_done = []
+
+    def step(self, i):
+        import pyoracle  # noqa: F401
+        b = i % self.R
+        sl = slice(b * self.S, (b + 1) * self.S)
+        # crypt only batch b's sessions (others keep their state)
+        sub_off = self.w.off.copy()
+        sub_len = np.zeros_like(self.w.length)
+        sub_len[sl] = self.w.length[sl]
+        self.ob.crypt(self.w.payload, sub_off, sub_len)
+        self.steps_done.append(i)
+
+    def sync(self):
+        pass
+
+    def check(self):
+        pass
+
+    def timed_steps(self, first, k):
+        import time
+        out = []
+        for i in range(first, first + k):
+            t0 = time.perf_counter()
+            self.step(i)
+            out.append((time.perf_counter() - t0) * 1e3)
+        return out
+
+
+def _worker(rank, ws, port, q, workload, steps, warmup, footprint):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import bench
+    bench.CONFIG_SHAPES["tiny"] = (256, 64)
+    bench.CONFIG_TEXT["tiny"] = "256 sessions x 64 B (test shape)"
+    args = bench.parse(["--workload", "cfg2", "--steps", str(steps), "--warmup", str(warmup),
+                        "--footprint-mib", str(footprint), "--cpu-seconds", "0"])
+    args.workload = workload
+    res, runner = bench.run_bench(args, ws, rank, rank, backend="gloo", make_runner=OracleRunner)
+    q.put((rank, res, runner.first, runner.S * runner.R,
+           hashlib.sha256(runner.w.payload.tobytes()).hexdigest(), len(runner.steps_done)))
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_sharding_and_aggregate():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ws, steps, warmup = 2, 3, 1
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, q, "tiny", steps, warmup, 0))
+             for r in range(ws)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(ws)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    got.sort()
+    (r0, res, first0, n0, dig0, nsteps0), (r1, res1, first1, n1, dig1, nsteps1) = got
+    assert res1 is None and res is not None
+    # disjoint, contiguous shards of global session ids
+    assert (first0, first1) == (0, n0) and n0 == n1
+    assert nsteps0 == nsteps1 == steps + warmup
+    # each rank's result equals a single-process run over the same global ids
+    sys.path.insert(0, str(ROOT / "oracle"))
+    for first, n, dig in ((first0, n0, dig0), (first1, n1, dig1)):
+        r = OracleRunner(256, 64, 1, first)
+        for i in range(steps + warmup):
+            r.step(i)
+        assert hashlib.sha256(r.w.payload.tobytes()).hexdigest() == dig
+    # aggregate: whole-job payload over the max rank time, weak scaling
+    assert res["n_gpus"] == 2 and res["scaling"] == "weak"
+    total = ws * steps * 256 * 64
+    assert abs(res["value"] - total / (res["ms_per_step"] * steps * 1e-3) / 2**30) < 1e-3 * res["value"] + 1e-6
+    assert res["config"]["global_sessions_per_step"] == 512

@@ -214,6 +214,33 @@ __global__ void __launch_bounds__(256) mem_kernel(uint64_t *out, uint8_t *buf, i
     if ((threadIdx.x & 63) == 0) out[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;
 }
 
+
+// ------------------------------- 6. load-only / store-only / DMA addressing cost
+// 8 waves/CU, each lane streams 16 B accesses; session stride 1 KiB.
+//  K 0: scattered dwordx4 loads (lane = session)      K 1: scattered dwordx4 stores
+//  K 2: quad-coalesced dwordx4 loads                  K 3: quad-coalesced dwordx4 stores
+//  K 4: quad-coalesced global_load_lds_dwordx4 (LDS-DMA, 4 KiB staging per wave)
+template <int K>
+__global__ void __launch_bounds__(256) addr_kernel(uint64_t *out, uint8_t *buf, int nblk) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[16384];
+    const size_t gtid = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (int blk = 0; blk < nblk; ++blk) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint8_t *p;
+            if (K == 0 || K == 1) p = buf + gtid * 1024 + blk * 64 + q * 16;
+            else p = buf + ((gtid & ~(size_t)63) + q * 16 + lane / 4) * 1024 + blk * 64 + (lane & 3) * 16;
+            if (K == 0 || K == 2) { uint4 v = *(uint4 *)p; acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w; }
+            if (K == 1 || K == 3) *(uint4 *)p = make_uint4(blk, q, lane, 7);
+            if (K == 4) __builtin_amdgcn_global_load_lds((const void *)p, (void *)(stage + wave * 4096 + q * 1024), 16, 0, 0);
+        }
+        if (K == 4 && (blk & 7) == 7) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); acc.x ^= stage[threadIdx.x * 16]; }
+    }
+    if (acc.x == 0x12345 && acc.y == 7) out[1 << 20] = acc.z;
+}
+
 static double median(std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; }
 
 int main() {
@@ -342,6 +369,34 @@ int main() {
             double bytes = (double)sessions * nblk * 64;
             printf(" \"mem_%s\": {\"ms\": %.4f, \"payload_GBps\": %.1f, \"rw_GBps\": %.1f},\n", p.name, ms,
                    bytes / (ms * 1e-3) / 1e9, 2 * bytes / (ms * 1e-3) / 1e9);
+        }
+        CHECK(hipFree(buf));
+    }
+
+    // 6. addressing cost of scattered vs quad-coalesced loads/stores and LDS-DMA
+    {
+        const int nblk = 16, blocks = ncu * 2 * 4;
+        const size_t sessions = (size_t)blocks * 256;
+        uint8_t *buf; CHECK(hipMalloc(&buf, sessions * 1024 + 4096));
+        CHECK(hipMemset(buf, 1, sessions * 1024 + 4096));
+        const char *kn[] = {"scatter_load", "scatter_store", "quad_load", "quad_store", "quad_lds_dma_load"};
+        for (int kk = 0; kk < 5; ++kk) {
+            auto launch = [&]() {
+                switch (kk) {
+                case 0: hipLaunchKernelGGL(addr_kernel<0>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
+                case 1: hipLaunchKernelGGL(addr_kernel<1>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
+                case 2: hipLaunchKernelGGL(addr_kernel<2>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
+                case 3: hipLaunchKernelGGL(addr_kernel<3>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
+                case 4: hipLaunchKernelGGL(addr_kernel<4>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
+                }
+            };
+            launch(); CHECK(hipDeviceSynchronize());
+            CHECK(hipEventRecord(e0)); launch(); CHECK(hipEventRecord(e1)); CHECK(hipEventSynchronize(e1));
+            float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
+            double bytes = (double)sessions * nblk * 64;
+            double instr_per_cu = (double)blocks * 4 * nblk * 4 / ncu;   // wave-instructions per CU
+            printf(" \"addr_%s\": {\"ms\": %.4f, \"GBps\": %.1f, \"ns_per_wave_instr_per_cu\": %.2f},\n", kn[kk], ms,
+                   bytes / (ms * 1e-3) / 1e9, ms * 1e6 / instr_per_cu);
         }
         CHECK(hipFree(buf));
     }

@@ -13,6 +13,7 @@
 
 struct zrc4_ctx {
     int device;
+    int num_cus;
     uint32_t capacity;      // multiple of 256
     uint8_t *arena;         // capacity/256 groups x 64 KiB S-box images
     uint16_t *xy;           // per slot: x | y << 8
@@ -65,8 +66,19 @@ int launch_crypt(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, uint8_t 
     if (n == 0) return ZRC4_OK;
     if (!ids && (uint64_t)first_slot + n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
     const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
-    hipLaunchKernelGGL(zrc4::crypt_kernel, dim3(grid), dim3(zrc4::kGroup), 0, s, c->arena,
-                       c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err);
+#if ZRC4_STAGED_STORE >= 0
+    const bool staged = ZRC4_STAGED_STORE != 0;
+#else
+    const bool staged = grid > (uint32_t)c->num_cus;   // >1 workgroup per CU
+#endif
+    if (staged)
+        hipLaunchKernelGGL(zrc4::crypt_kernel<true>, dim3(grid), dim3(zrc4::kGroup), 0, s,
+                           c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
+                           c->err);
+    else
+        hipLaunchKernelGGL(zrc4::crypt_kernel<false>, dim3(grid), dim3(zrc4::kGroup), 0, s,
+                           c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
+                           c->err);
     return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
 }
 
@@ -113,6 +125,7 @@ int zrc4_create(zrc4_ctx **out, int device, uint32_t capacity)
     zrc4_ctx *c = new (std::nothrow) zrc4_ctx();
     if (!c) return ZRC4_ERR_OUT_OF_MEMORY;
     c->device = device;
+    c->num_cus = prop.multiProcessorCount;
     const uint64_t cap = ((uint64_t)capacity + 255u) & ~(uint64_t)255u;
     if (cap > 0xFFFFFF00ull) { delete c; return ZRC4_ERR_INVALID_ARG; }
     c->capacity = (uint32_t)cap;

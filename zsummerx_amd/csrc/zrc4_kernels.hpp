@@ -289,6 +289,111 @@ __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st, uint8_t *
     for (uint32_t i = 0; i < rem; ++i) t[i] ^= (uint8_t)prga_step(S, st);
 }
 
+// Store path per launch (host picks, zrc4.hip): staged stores pay off when
+// two workgroups share a CU (store-throughput bound); with one wave per SIMD
+// the kernel is chain-latency bound and the staging round trip costs more.
+// ZRC4_STAGED_STORE=0/1 forces one path for A/B builds.
+#ifndef ZRC4_STAGED_STORE
+#define ZRC4_STAGED_STORE -1
+#endif
+
+constexpr int kStageBytes = 4096;                  // per wave: one 64-B block per lane
+constexpr int kSmemBytes = kGroupBytes + 4 * kStageBytes;   // 80 KiB: 2 workgroups per CU
+
+// global-address-space views (pointers rebuilt from shuffled integers would
+// otherwise become flat accesses, which force vmcnt(0)+lgkmcnt(0) waits)
+typedef __attribute__((address_space(1))) uint8_t gu8;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint32_t o = __shfl_xor(v, m, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// Staged-store message loop (the default).
+//
+// Measured on gfx950 (tools/ubench/lds_ubench.hip, 8 waves/CU): per-lane
+// scattered 16-B loads stream at 5.5 TB/s, but per-lane scattered 16-B
+// STORES (64 lines per wave-instruction) at only 0.96 TB/s, against 2.4 TB/s
+// when each 4-lane quad writes 64 contiguous bytes.  So loads stay per lane
+// (prefetched one block ahead in registers) while results go through a
+// 4 KiB per-wave LDS staging slot and leave as quad-coalesced stores: lane l
+// of store instruction q writes 16 B of session 16q + l/4.  The block loop is
+// wave-uniform (to the wave's longest message) so every lane can store on
+// behalf of others; owner lanes past their own end skip the keystream.
+// Owner s writes chunk c at slot s*64 + (c ^ ((s>>1)&3))*16: conflict-free for
+// ds_write_b128's 8-lane groups; store lanes read linearly (conflict-free).
+__device__ __forceinline__ void crypt_message_staged(uint8_t *S, uint8_t *stage, Rc4Lane &st,
+                                                     uint8_t *msg, uint32_t len, uint4 (&A)[4],
+                                                     bool pre)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t head = head_bytes(msg, len);
+    for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
+    msg += head;
+    len -= head;
+    uint4 *p = reinterpret_cast<uint4 *>(msg);
+    const uint32_t nblk = len >> 6;
+
+    // store-role addressing: session 16q + lane/4 of this wave, for q = 0..3
+    const uint32_t wmax = wave_max(nblk);
+    uint32_t snb[4];
+    gu8 *sbase[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int src = 16 * q + (int)(lane >> 2);
+        snb[q] = __shfl(nblk, src, 64);
+        const uint64_t b = __shfl((uint64_t)(uintptr_t)msg, src, 64);
+        const uint32_t c = (lane & 3u) ^ (((uint32_t)src >> 1) & 3u);
+        sbase[q] = reinterpret_cast<gu8 *>((uintptr_t)b) + c * 16u;
+    }
+    uint4 *wslot = reinterpret_cast<uint4 *>(stage + lane * 64u);
+    const uint32_t wsw = (lane >> 1) & 3u;
+    const uint4 *rslot = reinterpret_cast<const uint4 *>(stage + lane * 16u);
+
+    uint4 B[4];
+    if (!pre && nblk) load64(A, p);
+    auto block = [&](uint32_t blk, uint4(&cur)[4], uint4(&nxt)[4]) {
+        if (blk < nblk) {
+            load64(nxt, (blk + 1 < nblk) ? p + 4 * (blk + 1) : p + 4 * blk);
+            xor64_asm(st, cur);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) wslot[c ^ wsw] = cur[c];
+        }
+        // LDS ops of one wave execute in order; a compiler-only barrier keeps
+        // the staging reads below the other lanes' writes (no wait emitted).
+        asm volatile("" ::: "memory");
+        uint4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = rslot[q * 64];     // all reads, then stores
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (blk < snb[q])
+                *reinterpret_cast<gu32x4 *>(sbase[q] + blk * 64u) = u32x4{v[q].x, v[q].y, v[q].z, v[q].w};
+        asm volatile("" ::: "memory");
+    };
+    for (uint32_t blk = 0; blk < wmax; blk += 2) {
+        block(blk, A, B);
+        if (blk + 1 >= wmax) break;
+        block(blk + 1, B, A);
+    }
+    p += 4 * nblk;
+    uint32_t rem = len & 63u;
+    while (rem >= 16u) {
+        *p = xor16(S, st, *p);
+        ++p;
+        rem -= 16u;
+    }
+    uint8_t *t = reinterpret_cast<uint8_t *>(p);
+    for (uint32_t i = 0; i < rem; ++i) t[i] ^= (uint8_t)prga_step(S, st);
+}
+
 // Which slot batch entry e maps to, and whether workgroup w owns one whole
 // aligned 256-slot group g (then state moves as a coalesced 64 KiB image).
 //   ids == NULL : slot = first_slot + e; whole iff first_slot % 256 == 0
@@ -304,6 +409,7 @@ __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st, uint8_t *
 // first (group image, len/off/xy, the first payload block) so it costs about
 // two HBM round trips instead of a dependent chain of them.
 // ---------------------------------------------------------------------------
+template <bool STAGED>
 __global__ void __launch_bounds__(256, 2)
 crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
              const uint32_t *__restrict__ ids, uint32_t first_slot,
@@ -311,7 +417,10 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
              const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
              uint32_t *__restrict__ err)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t S[kGroupBytes];
+    // one LDS object: 64 KiB S-box image + 4 x 4 KiB store staging (80 KiB,
+    // so two workgroups fill the CU's 160 KiB).  No other __shared__ object.
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kSmemBytes : kGroupBytes + 16];
+    uint8_t *S = smem;
 
     const uint32_t j = threadIdx.x;
     const uint32_t e = blockIdx.x * kGroup + j;
@@ -335,7 +444,14 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     } else {
         const uint32_t first = ids[blockIdx.x * kGroup];
         g = first >> 8;
-        whole = __syncthreads_and(active && slot == ((first & ~255u) + j) && (first & 255u) == 0u);
+        // workgroup AND through one staging word (no extra LDS allocation)
+        volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(smem + kGroupBytes);
+        if (j == 0) *flag = 1u;
+        __syncthreads();
+        if (!(active && slot == ((first & ~255u) + j) && (first & 255u) == 0u)) *flag = 0u;
+        __syncthreads();
+        whole = *flag != 0u;
+        __syncthreads();
     }
 
     const uint32_t col = col_of(j);
@@ -357,7 +473,24 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         if (active && mylen) gather_column(S, col, arena, slot);
     }
 
-    if (active && mylen) {
+    if (STAGED) {
+    // Every lane of a wave takes part in the staged stores, so the message
+    // loop runs for all lanes (an idle lane has len 0: no keystream, no state
+    // change) and only the state write-back is predicated.
+    {
+        const uint32_t x = sxy & 255u, y = sxy >> 8;
+        Rc4Lane st;
+        st.col = col;
+        st.x0 = (((x + 1u) & 255u) << 8) | col;
+        st.a0 = S[st.x0];
+        st.ya = (y << 8) | col;
+        st.ta = col;
+        st.x1 = col;
+        crypt_message_staged(S, smem + kGroupBytes + (j >> 6) * kStageBytes, st, msg, mylen, A, pre);
+        if (active && mylen)
+            xy[slot] = (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
+    }
+    } else if (active && mylen) {
         const uint32_t x = sxy & 255u, y = sxy >> 8;
         Rc4Lane st;
         st.col = col;
