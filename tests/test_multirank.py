@@ -114,5 +114,6 @@ def test_two_rank_gloo_sharding_and_aggregate():
     # aggregate: whole-job payload over the max rank time, weak scaling
     assert res["n_gpus"] == 2 and res["scaling"] == "weak"
     total = ws * steps * 256 * 64
-    assert abs(res["value"] - total / (res["ms_per_step"] * steps * 1e-3) / 2**30) < 1e-3 * res["value"] + 1e-6
+    expect = total / (res["ms_per_step"] * steps * 1e-3) / 2**30   # both fields are rounded
+    assert abs(res["value"] - expect) <= 0.02 * expect + 2e-3
     assert res["config"]["global_sessions_per_step"] == 512
