@@ -32,10 +32,16 @@ for wl in $WLS; do
   rc=$?; cat $OUT/bench_$wl.json; stop_on_fault $rc bench-$wl
 done
 
+for wl in $WLS; do
+  timeout -k 10 200 python bench.py --workload $wl --host-inclusive --steps 20 --warmup 3 \
+      > $OUT/hostinc_$wl.json 2> $OUT/hostinc_$wl.err
+  rc=$?; cat $OUT/hostinc_$wl.json; stop_on_fault $rc hostinc-$wl
+done
+
 cd /tmp && export TMPDIR=/tmp
 for wl in $WLS; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof_$wl -o run \
-      --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --workload $wl --steps 50 --warmup 5 --cpu-seconds 0 \
+      --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --workload $wl --steps 200 --warmup 20 --cpu-seconds 0 \
       > $GRAFT_REPO_ROOT/$OUT/prof_$wl.log 2>&1
   rc=$?; stop_on_fault $rc rocprof-$wl
 done

@@ -66,3 +66,25 @@ def test_no_device_is_a_loud_error(built):
     with pytest.raises(ZRC4Error) as ei:
         Context(0, 256)
     assert ei.value.code == -2
+
+
+def _build_cpp_test(tmp_path):
+    exe = tmp_path / "test_rc4_mirror"
+    lib_dir = ROOT / "zsummerx_amd"
+    cmd = ["g++", "-O2", "-std=c++17", f"-I{ROOT / 'include'}", str(ROOT / "tests" / "cpp" / "test_rc4_mirror.cpp"),
+           f"-L{lib_dir}", "-lzrc4", f"-Wl,-rpath,{lib_dir}", "-o", str(exe)]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+def test_cpp_mirror_header_compiles_and_links(built, tmp_path):
+    """The reference-shaped C++ header compiles against the C-ABI and links."""
+    assert _build_cpp_test(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_cpp_mirror_runs_on_gpu(built, tmp_path):
+    exe = _build_cpp_test(tmp_path)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "ok" in out.stdout
