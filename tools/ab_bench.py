@@ -30,6 +30,7 @@ SHAPES = {"cfg2": (4096, 1024), "cfg3": (65536, 256), "cfg4": (1024, 65536), "cf
 
 
 def parse_variant(v: str):
+    """name[@gitrev]:DEF=v,DEF2=v"""
     name, _, defs = v.partition(":")
     d = {}
     for kv in filter(None, defs.split(",")):
@@ -52,7 +53,8 @@ def main():
     variants = []
     for v in args.variant:
         name, defs = parse_variant(v)
-        variants.append((name, build.build_variant(name, defs)))
+        name, _, rev = name.partition("@")
+        variants.append((name, build.build_variant(name, defs, rev or None)))
     if args.build_only:
         print("built", [str(p) for _, p in variants])
         return

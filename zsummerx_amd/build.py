@@ -49,15 +49,30 @@ def build_lib(force: bool = False, extra_flags=()) -> Path:
     return LIB
 
 
-def build_variant(name: str, defines: dict) -> Path:
-    """A/B builds: the same library under another name with -D switches
-    (tools/ab_bench.py loads several side by side in one process)."""
+def build_variant(name: str, defines: dict, rev: str | None = None) -> Path:
+    """A/B builds: the same library under another name with -D switches, or
+    the sources of git revision `rev` (tools/ab_bench.py loads several side by
+    side in one process)."""
     out = PKG / f"libzrc4_{name}.so"
-    if _stale(out, HIP_DEPS):
+    srcs, inc, deps = HIP_SOURCES, ROOT / "include", HIP_DEPS
+    if rev:
+        tree = BUILD / f"rev_{name}"
+        (tree / "csrc").mkdir(parents=True, exist_ok=True)
+        (tree / "include").mkdir(parents=True, exist_ok=True)
+        for rel, dst in (("zsummerx_amd/csrc/zrc4.hip", tree / "csrc" / "zrc4.hip"),
+                         ("zsummerx_amd/csrc/zrc4_kernels.hpp", tree / "csrc" / "zrc4_kernels.hpp"),
+                         ("include/zrc4.h", tree / "include" / "zrc4.h")):
+            blob = subprocess.run(["git", "show", f"{rev}:{rel}"], cwd=ROOT, check=True,
+                                  capture_output=True).stdout
+            if not dst.exists() or dst.read_bytes() != blob:
+                dst.write_bytes(blob)
+        srcs, inc = [tree / "csrc" / "zrc4.hip"], tree / "include"
+        deps = [tree / "csrc" / "zrc4.hip", tree / "csrc" / "zrc4_kernels.hpp", inc / "zrc4.h"]
+    if _stale(out, deps):
         BUILD.mkdir(exist_ok=True)
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               f"-I{ROOT / 'include'}", *[f"-D{k}={v}" for k, v in defines.items()],
-               "-o", str(out), *map(str, HIP_SOURCES)]
+               f"-I{inc}", *[f"-D{k}={v}" for k, v in defines.items()],
+               "-o", str(out), *map(str, srcs)]
         subprocess.run(cmd, check=True, cwd=BUILD)
     return out
 
