@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--footprint-mib", type=int, default=640)
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="timing-only ablation builds (outputs differ)")
     args = ap.parse_args()
 
     from zsummerx_amd import build
@@ -103,7 +104,7 @@ def main():
             _capi.check(lib.zrc4_sync(h, st))
             if ref is None:
                 ref = buf
-            elif not torch.equal(ref, buf):
+            elif not args.no_check and not torch.equal(ref, buf):
                 raise SystemExit(f"variant {name} output differs from {libs[0][0]} on {wl}")
         times = {name: [] for name, _ in libs}
         step = 1

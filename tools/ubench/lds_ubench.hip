@@ -234,6 +234,14 @@ __global__ void __launch_bounds__(256) addr_kernel(uint64_t *out, uint8_t *buf, 
             else p = buf + ((gtid & ~(size_t)63) + q * 16 + lane / 4) * 1024 + blk * 64 + (lane & 3) * 16;
             if (K == 0 || K == 2) { uint4 v = *(uint4 *)p; acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w; }
             if (K == 1 || K == 3) *(uint4 *)p = make_uint4(blk, q, lane, 7);
+            if (K == 5) {   // oct-coalesced: 8 lanes write 128 contiguous B of one session (2 blocks)
+                uint8_t *po = buf + ((gtid & ~(size_t)63) + q * 8 + lane / 8 + (blk & 1) * 32) * 1024 + (blk >> 1) * 128 + (lane & 7) * 16;
+                *(uint4 *)po = make_uint4(blk, q, lane, 7);
+            }
+            if (K == 6) {   // full-line per lane pair... 16 lanes x 64 B: 1 KiB contiguous (one session per instruction)
+                uint8_t *pf = buf + ((gtid & ~(size_t)63) + q * 16 + (blk % 16)) * 1024 + lane * 16;
+                *(uint4 *)pf = make_uint4(blk, q, lane, 7);
+            }
             if (K == 4) __builtin_amdgcn_global_load_lds((const void *)p, (void *)(stage + wave * 4096 + q * 1024), 16, 0, 0);
         }
         if (K == 4 && (blk & 7) == 7) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); acc.x ^= stage[threadIdx.x * 16]; }
@@ -379,8 +387,8 @@ int main() {
         const size_t sessions = (size_t)blocks * 256;
         uint8_t *buf; CHECK(hipMalloc(&buf, sessions * 1024 + 4096));
         CHECK(hipMemset(buf, 1, sessions * 1024 + 4096));
-        const char *kn[] = {"scatter_load", "scatter_store", "quad_load", "quad_store", "quad_lds_dma_load"};
-        for (int kk = 0; kk < 5; ++kk) {
+        const char *kn[] = {"scatter_load", "scatter_store", "quad_load", "quad_store", "quad_lds_dma_load", "oct_store", "kib_store"};
+        for (int kk = 0; kk < 7; ++kk) {
             auto launch = [&]() {
                 switch (kk) {
                 case 0: hipLaunchKernelGGL(addr_kernel<0>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
@@ -388,6 +396,8 @@ int main() {
                 case 2: hipLaunchKernelGGL(addr_kernel<2>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
                 case 3: hipLaunchKernelGGL(addr_kernel<3>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
                 case 4: hipLaunchKernelGGL(addr_kernel<4>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
+                case 5: hipLaunchKernelGGL(addr_kernel<5>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
+                case 6: hipLaunchKernelGGL(addr_kernel<6>, dim3(blocks), dim3(256), 0, 0, d_out, buf, nblk); break;
                 }
             };
             launch(); CHECK(hipDeviceSynchronize());

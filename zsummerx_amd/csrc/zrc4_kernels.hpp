@@ -331,10 +331,24 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 // ds_write_b128's 8-lane groups; store lanes read linearly (conflict-free).
 __device__ __forceinline__ void crypt_message_staged(uint8_t *S, uint8_t *stage, Rc4Lane &st,
                                                      uint8_t *msg, uint32_t len, uint4 (&A)[4],
-                                                     bool pre)
+                                                     bool pre_in)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t head = head_bytes(msg, len);
+#ifndef ZRC4_STAGGER
+#define ZRC4_STAGGER 0
+#endif
+#ifndef ZRC4_ABLATE
+#define ZRC4_ABLATE 0      // timing-only builds: 1 no stores, 2 no loads, 3 neither, 4 no staging/stores
+#endif
+    bool pre = pre_in;
+    uint32_t head = head_bytes(msg, len);
+    // Stagger (A/B knob): odd waves run half a block through the C step first,
+    // so their memory phases fall inside the even waves' keystream phases.
+    if (ZRC4_STAGGER && ((threadIdx.x >> 6) & 1u)) {
+        const uint32_t extra = len - head < 32u ? len - head : 32u;
+        head += extra;
+        pre = false;                      // the caller's preload started at offset 0
+    }
     for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
     msg += head;
     len -= head;
@@ -361,21 +375,28 @@ __device__ __forceinline__ void crypt_message_staged(uint8_t *S, uint8_t *stage,
     if (!pre && nblk) load64(A, p);
     auto block = [&](uint32_t blk, uint4(&cur)[4], uint4(&nxt)[4]) {
         if (blk < nblk) {
-            load64(nxt, (blk + 1 < nblk) ? p + 4 * (blk + 1) : p + 4 * blk);
+            if (!(ZRC4_ABLATE & 2)) load64(nxt, (blk + 1 < nblk) ? p + 4 * (blk + 1) : p + 4 * blk);
             xor64_asm(st, cur);
+            if (ZRC4_ABLATE != 4) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) wslot[c ^ wsw] = cur[c];
+                for (int c = 0; c < 4; ++c) wslot[c ^ wsw] = cur[c];
+            }
         }
+        if (ZRC4_ABLATE == 4) return;
         // LDS ops of one wave execute in order; a compiler-only barrier keeps
         // the staging reads below the other lanes' writes (no wait emitted).
         asm volatile("" ::: "memory");
         uint4 v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = rslot[q * 64];     // all reads, then stores
+        if (!(ZRC4_ABLATE & 1)) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (blk < snb[q])
-                *reinterpret_cast<gu32x4 *>(sbase[q] + blk * 64u) = u32x4{v[q].x, v[q].y, v[q].z, v[q].w};
+            for (int q = 0; q < 4; ++q)
+                if (blk < snb[q])
+                    *reinterpret_cast<gu32x4 *>(sbase[q] + blk * 64u) = u32x4{v[q].x, v[q].y, v[q].z, v[q].w};
+        } else {
+            asm volatile("" :: "v"(v[0].x), "v"(v[1].x), "v"(v[2].x), "v"(v[3].x));
+        }
         asm volatile("" ::: "memory");
     };
     for (uint32_t blk = 0; blk < wmax; blk += 2) {
@@ -384,6 +405,139 @@ __device__ __forceinline__ void crypt_message_staged(uint8_t *S, uint8_t *stage,
         block(blk + 1, B, A);
     }
     p += 4 * nblk;
+    uint32_t rem = len & 63u;
+    while (rem >= 16u) {
+        *p = xor16(S, st, *p);
+        ++p;
+        rem -= 16u;
+    }
+    uint8_t *t = reinterpret_cast<uint8_t *>(p);
+    for (uint32_t i = 0; i < rem; ++i) t[i] ^= (uint8_t)prga_step(S, st);
+}
+
+#ifndef ZRC4_LINE_STORE
+#define ZRC4_LINE_STORE 1
+#endif
+
+__device__ __forceinline__ void load4(uint4 *q, const uint4 *p)
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = p[i];
+}
+
+__device__ __forceinline__ void xor64_asm_p(Rc4Lane &st, uint4 *q)
+{
+    xor64_asm(st, *reinterpret_cast<uint4(*)[4]>(q));
+}
+
+__device__ __forceinline__ void swap_halves(uint4 *lo, uint4 *hi)
+{
+    // v_permlane32_swap: lanes 32-63 of `lo` <-> lanes 0-31 of `hi`
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        auto rx = __builtin_amdgcn_permlane32_swap(lo[i].x, hi[i].x, false, false);
+        auto ry = __builtin_amdgcn_permlane32_swap(lo[i].y, hi[i].y, false, false);
+        auto rz = __builtin_amdgcn_permlane32_swap(lo[i].z, hi[i].z, false, false);
+        auto rw = __builtin_amdgcn_permlane32_swap(lo[i].w, hi[i].w, false, false);
+        lo[i] = make_uint4(rx[0], ry[0], rz[0], rw[0]);
+        hi[i] = make_uint4(rx[1], ry[1], rz[1], rw[1]);
+    }
+}
+
+// Staged message loop with WHOLE-LINE stores (the default staged path).
+//
+// Measured on gfx950 (tools/ubench/lds_ubench.hip, 8 waves/CU): stores where
+// 8 lanes write one full 128-B line run at 5.65 TB/s, 4-lane 64-B pieces at
+// 2.36 TB/s, per-lane 16-B pieces at 0.96 TB/s.  So results leave in whole
+// lines: a lane keeps two consecutive 64-B blocks (b, b+1) = one line of its
+// session, a v_permlane32_swap per dword hands block b+1 of the lower half to
+// the upper half and block b of the upper half to the lower half, and the
+// 4 KiB per-wave staging slot then holds 32 full lines per round (all 64 lanes
+// write 64 B each, two rounds per block pair).  Store lanes read the slot
+// linearly and write 8 sessions x 128 B per instruction.  The 16-B slot of
+// line chunk m of staging row r is (m + r) & 7: conflict-free ds_write_b128
+// for the 8-lane groups (distinct rows), conflict-free linear reads.
+// Loads stay per lane (5.5 TB/s), one block pair ahead.
+__device__ __forceinline__ void crypt_message_lines(uint8_t *S, uint8_t *stage, Rc4Lane &st,
+                                                    uint8_t *msg, uint32_t len, uint4 (&A)[4],
+                                                    bool pre)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t head = head_bytes(msg, len);
+    for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
+    msg += head;
+    len -= head;
+    uint4 *p = reinterpret_cast<uint4 *>(msg);
+    const uint32_t nblk = len >> 6;
+    const uint32_t last = nblk ? nblk - 1u : 0u;
+    const uint32_t wmax = wave_max(nblk);
+
+    // store role: round r, instruction q -> session 32r + 8q + lane/8, slot lane&7
+    uint32_t snb[2][4];
+    gu8 *sbase[2][4];
+    uint32_t smask[2][4];  // which line chunk this lane stores (byte offset m*16)
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int src = 32 * r + 8 * q + (int)(lane >> 3);
+            snb[r][q] = __shfl(nblk, src, 64);
+            const uint64_t b = __shfl((uint64_t)(uintptr_t)msg, src, 64);
+            const uint32_t row = (uint32_t)src & 31u;
+            const uint32_t m = ((lane & 7u) - row) & 7u;       // slot = (m + row) & 7
+            smask[r][q] = m;
+            sbase[r][q] = reinterpret_cast<gu8 *>((uintptr_t)b) + m * 16u;
+        }
+    // write role: row = lane & 31, half h = lane >> 5 (chunks 4h .. 4h+3)
+    const uint32_t wrow = lane & 31u, wh = lane >> 5;
+    uint8_t *wrow_base = stage + wrow * 128u;
+    const uint4 *rslot = reinterpret_cast<const uint4 *>(stage + lane * 16u);
+
+    auto stage_round = [&](int r, const uint4 *blk4, uint32_t b) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t m = 4u * wh + (uint32_t)c;
+            *reinterpret_cast<uint4 *>(wrow_base + (((m + wrow) & 7u) * 16u)) = blk4[c];
+        }
+        asm volatile("" ::: "memory");
+        uint4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = rslot[q * 64];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            // chunk m lies in block b + (m >= 4) of the pair
+            if (b + (smask[r][q] >> 2) < snb[r][q])
+                *reinterpret_cast<gu32x4 *>(sbase[r][q] + b * 64u) = u32x4{v[q].x, v[q].y, v[q].z, v[q].w};
+        }
+        asm volatile("" ::: "memory");
+    };
+
+    uint4 A1[4], B0[4], B1[4];
+    auto load_pair = [&](uint4 *d0, uint4 *d1, uint32_t b) {
+        const uint32_t b0 = b < last ? b : last, b1 = b + 1u < last ? b + 1u : last;
+        load4(d0, p + 4u * b0);
+        load4(d1, p + 4u * b1);
+    };
+    if (nblk) {
+        if (!pre) load4(A, p);
+        load4(A1, p + 4u * (1u < last ? 1u : last));
+    }
+    auto pair = [&](uint32_t b, uint4 *x0, uint4 *x1) {
+        if (b < nblk) xor64_asm_p(st, x0);
+        if (b + 1u < nblk) xor64_asm_p(st, x1);
+        swap_halves(x0, x1);
+        stage_round(0, x0, b);
+        stage_round(1, x1, b);
+    };
+    for (uint32_t b = 0; b < wmax; b += 4) {
+        if (nblk) load_pair(B0, B1, b + 2u);
+        pair(b, A, A1);
+        if (b + 2u >= wmax) break;
+        if (nblk) load_pair(A, A1, b + 4u);
+        pair(b + 2u, B0, B1);
+    }
+
+    p += 4u * nblk;
     uint32_t rem = len & 63u;
     while (rem >= 16u) {
         *p = xor16(S, st, *p);
@@ -486,7 +640,10 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         st.ya = (y << 8) | col;
         st.ta = col;
         st.x1 = col;
-        crypt_message_staged(S, smem + kGroupBytes + (j >> 6) * kStageBytes, st, msg, mylen, A, pre);
+        if (ZRC4_LINE_STORE)
+            crypt_message_lines(S, smem + kGroupBytes + (j >> 6) * kStageBytes, st, msg, mylen, A, pre);
+        else
+            crypt_message_staged(S, smem + kGroupBytes + (j >> 6) * kStageBytes, st, msg, mylen, A, pre);
         if (active && mylen)
             xy[slot] = (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
     }
