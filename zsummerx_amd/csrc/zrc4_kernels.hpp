@@ -460,7 +460,7 @@ __device__ __forceinline__ void swap_halves(uint4 *lo, uint4 *hi)
 // Loads stay per lane (5.5 TB/s), one block pair ahead.
 __device__ __forceinline__ void crypt_message_lines(uint8_t *S, uint8_t *stage, Rc4Lane &st,
                                                     uint8_t *msg, uint32_t len, uint4 (&A)[4],
-                                                    bool pre)
+                                                    bool pre, uint4 *A1pre = nullptr)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t head = head_bytes(msg, len);
@@ -513,6 +513,10 @@ __device__ __forceinline__ void crypt_message_lines(uint8_t *S, uint8_t *stage, 
     };
 
     uint4 A1[4], B0[4], B1[4];
+    if (A1pre) {   // both blocks of the first pair were prefetched by the caller
+#pragma unroll
+        for (int i = 0; i < 4; ++i) A1[i] = A1pre[i];
+    }
     auto load_pair = [&](uint4 *d0, uint4 *d1, uint32_t b) {
         const uint32_t b0 = b < last ? b : last, b1 = b + 1u < last ? b + 1u : last;
         load4(d0, p + 4u * b0);
@@ -520,7 +524,7 @@ __device__ __forceinline__ void crypt_message_lines(uint8_t *S, uint8_t *stage, 
     };
     if (nblk) {
         if (!pre) load4(A, p);
-        load4(A1, p + 4u * (1u < last ? 1u : last));
+        if (!pre || !A1pre) load4(A1, p + 4u * (1u < last ? 1u : last));
     }
     auto pair = [&](uint32_t b, uint4 *x0, uint4 *x1) {
         if (b < nblk) xor64_asm_p(st, x0);
@@ -665,6 +669,98 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         lds_to_image(arena + (size_t)g * kGroupBytes, S);
     } else if (active && mylen) {
         scatter_column(arena, slot, S, col);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// crypt_persistent_kernel: the staged (whole-line store) kernel as a
+// persistent loop over whole 256-slot groups (contiguous range, group-aligned
+// first slot).  grid = min(groups, 2 per CU); workgroup w handles local groups
+// w, w + grid, ...  While group g's keystream runs, the next group's 64 KiB
+// image and lane data (len/off/xy) are prefetched into registers (prefetching
+// the first payload line too pushed the kernel past the register budget); at the hand-over each thread spills its own 16 image slices of
+// g and fills the prefetched slices of g' (4 at a time).  The state traffic of
+// every group but the first and last thereby overlaps keystream work instead
+// of arriving as synchronized fill/spill bursts between workgroup rounds.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256, 2)
+crypt_persistent_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
+                        uint32_t first_slot, uint8_t *__restrict__ payload,
+                        const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
+                        uint32_t n, uint32_t ngroups)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kSmemBytes];
+    uint8_t *S = smem;
+    uint4 *S4 = reinterpret_cast<uint4 *>(smem);
+    const uint32_t j = threadIdx.x;
+    const uint32_t col = col_of(j);
+    uint8_t *stage = smem + kGroupBytes + (j >> 6) * kStageBytes;
+    const uint32_t g0 = first_slot >> 8;
+
+    uint32_t gi = blockIdx.x;
+    if (gi >= ngroups) return;
+
+    uint4 img[16];
+    uint32_t nlen;
+    uint64_t noff;
+    uint16_t nxy;
+    auto prefetch = [&](uint32_t gl) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(arena + (size_t)(g0 + gl) * kGroupBytes);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) img[i] = src[i * 256 + j];
+        const uint32_t e = gl * kGroup + j;
+        const bool valid = e < n;
+        nlen = valid ? len[e] : 0u;
+        noff = valid ? off[e] : 0u;
+        nxy = (valid && nlen) ? xy[first_slot + e] : (uint16_t)0;
+    };
+
+    prefetch(gi);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) S4[i * 256 + j] = img[i];
+    __syncthreads();
+
+    while (true) {
+        // this group's lane data and first line, then the next group's prefetch
+        const uint32_t mylen = nlen;
+        uint8_t *msg = payload + noff;
+        const uint16_t sxy = nxy;
+        uint4 A[4];
+        const uint32_t gn = gi + gridDim.x;
+        const bool more = gn < ngroups;
+        if (more) prefetch(gn);
+
+        {
+            const uint32_t x = sxy & 255u, y = sxy >> 8;
+            Rc4Lane st;
+            st.col = col;
+            st.x0 = (((x + 1u) & 255u) << 8) | col;
+            st.a0 = S[st.x0];
+            st.ya = (y << 8) | col;
+            st.ta = col;
+            st.x1 = col;
+            crypt_message_lines(S, stage, st, msg, mylen, A, false);
+            if (mylen)
+                xy[first_slot + gi * kGroup + j] =
+                    (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
+        }
+        __syncthreads();
+        uint4 *dst = reinterpret_cast<uint4 *>(arena + (size_t)(g0 + gi) * kGroupBytes);
+#pragma unroll
+        for (int c = 0; c < 16; c += 4) {
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = S4[(c + k) * 256 + j];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dst[(c + k) * 256 + j] = v[k];
+            if (more) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) S4[(c + k) * 256 + j] = img[c + k];
+            }
+        }
+        if (!more) break;
+        __syncthreads();
+        gi = gn;
     }
 }
 
