@@ -168,6 +168,9 @@ class Batch:
         self.st = (OracleState * max(1, n))()
 
     def make_sbox(self, keys: np.ndarray, key_off: np.ndarray, key_len: np.ndarray) -> None:
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        key_off = np.ascontiguousarray(key_off, dtype=np.uint64)
+        key_len = np.ascontiguousarray(key_len, dtype=np.uint32)
         lib().oracle_make_sbox_batch(self.st, C.c_void_p(keys.ctypes.data),
                                      C.c_void_p(key_off.ctypes.data),
                                      C.c_void_p(key_len.ctypes.data), self.n)

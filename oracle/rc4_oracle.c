@@ -47,19 +47,17 @@ void oracle_make_sbox(oracle_rc4_state *st, const uint8_t *key, size_t keylen)
  * (:78-79, :91-92).  length <= 0 leaves data and state untouched. */
 void oracle_encryption(oracle_rc4_state *st, uint8_t *data, long length)
 {
-    unsigned x = (unsigned)st->x, y = (unsigned)st->y;
-    int *box = st->box;
+    int x = st->x, y = st->y;
     for (long i = 0; i < length; ++i) {
-        x = (x + 1) & 0xFFu;
-        int a = box[x];
-        y = (y + (unsigned)a) & 0xFFu;
-        int b = box[y];
-        box[x] = b;
-        box[y] = a;
-        data[i] ^= (uint8_t)box[(unsigned)(a + b) & 0xFFu];
+        x = (unsigned char)(x + 1);
+        int a = st->box[x];
+        y = (unsigned char)(y + a);
+        int b = st->box[x] = st->box[y];
+        st->box[y] = a;
+        data[i] ^= (uint8_t)st->box[(unsigned char)(a + b)];
     }
-    st->x = (int)x;
-    st->y = (int)y;
+    st->x = x;
+    st->y = y;
 }
 
 void oracle_make_sbox_batch(oracle_rc4_state *st, const uint8_t *keys,

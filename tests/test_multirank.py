@@ -59,13 +59,14 @@ class OracleRunner:
     def check(self):
         pass
 
-    def timed_steps(self, first, k):
+    def timed_steps(self, first, k, every=1):
         import time
         out = []
         for i in range(first, first + k):
             t0 = time.perf_counter()
             self.step(i)
-            out.append((time.perf_counter() - t0) * 1e3)
+            if (i - first) % every == 0:
+                out.append((time.perf_counter() - t0) * 1e3)
         return out
 
 
@@ -117,3 +118,7 @@ def test_two_rank_gloo_sharding_and_aggregate():
     expect = total / (res["ms_per_step"] * steps * 1e-3) / 2**30   # both fields are rounded
     assert abs(res["value"] - expect) <= 0.02 * expect + 2e-3
     assert res["config"]["global_sessions_per_step"] == 512
+    # per-GPU breakdown: one entry per rank, the slowest sets ms_per_step
+    assert [g["rank"] for g in res["per_gpu"]] == [0, 1]
+    slowest = min(g["payload_gibs"] for g in res["per_gpu"])
+    assert abs(slowest * ws - res["value"]) <= 0.05 * res["value"] + 2e-3

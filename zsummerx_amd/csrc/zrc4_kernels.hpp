@@ -338,7 +338,8 @@ __device__ __forceinline__ void crypt_message_staged(uint8_t *S, uint8_t *stage,
 #define ZRC4_STAGGER 0
 #endif
 #ifndef ZRC4_ABLATE
-#define ZRC4_ABLATE 0      // timing-only builds: 1 no stores, 2 no loads, 3 neither, 4 no staging/stores
+#define ZRC4_ABLATE 0      // timing-only builds: 1 no stores, 2 no loads, 3 neither, 4 no staging/stores,
+                           // +8 no group-image load, +16 no group-image store (crypt_kernel)
 #endif
     bool pre = pre_in;
     uint32_t head = head_bytes(msg, len);
@@ -617,6 +618,7 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     uint4 A[4];
     const bool pre = active && mylen >= 64u && head_bytes(msg, mylen) == 0u;
     if (whole) {
+        if (!(ZRC4_ABLATE & 8)) {
         uint4 img[16];
         const uint4 *src = reinterpret_cast<const uint4 *>(arena + (size_t)g * kGroupBytes);
 #pragma unroll
@@ -625,6 +627,9 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         uint4 *dst = reinterpret_cast<uint4 *>(S);
 #pragma unroll
         for (int i = 0; i < 16; ++i) dst[i * 256 + j] = img[i];
+        } else if (pre) {
+            load64(A, reinterpret_cast<const uint4 *>(msg));
+        }
         __syncthreads();
     } else {
         if (pre) load64(A, reinterpret_cast<const uint4 *>(msg));
@@ -666,7 +671,7 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 
     if (whole) {
         __syncthreads();
-        lds_to_image(arena + (size_t)g * kGroupBytes, S);
+        if (!(ZRC4_ABLATE & 16)) lds_to_image(arena + (size_t)g * kGroupBytes, S);
     } else if (active && mylen) {
         scatter_column(arena, slot, S, col);
     }
