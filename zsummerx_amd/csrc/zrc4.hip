@@ -71,14 +71,7 @@ int launch_crypt(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, uint8_t 
 #else
     const bool staged = grid > (uint32_t)c->num_cus;   // >1 workgroup per CU
 #endif
-#ifndef ZRC4_PERSIST
-#define ZRC4_PERSIST 0
-#endif
-    if (staged && ZRC4_PERSIST && !ids && (first_slot & 255u) == 0u) {
-        const uint32_t pgrid = grid < 2u * (uint32_t)c->num_cus ? grid : 2u * (uint32_t)c->num_cus;
-        hipLaunchKernelGGL(zrc4::crypt_persistent_kernel, dim3(pgrid), dim3(zrc4::kGroup), 0, s,
-                           c->arena, c->xy, first_slot, payload, off, len, n, grid);
-    } else if (staged)
+    if (staged)
         hipLaunchKernelGGL(zrc4::crypt_kernel<true>, dim3(grid), dim3(zrc4::kGroup), 0, s,
                            c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
                            c->err);

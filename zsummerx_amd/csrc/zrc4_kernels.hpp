@@ -30,6 +30,8 @@ constexpr int kGroupBytes = 256 * 256; // 64 KiB S-box image per group
 
 enum : uint32_t { kErrSlotRange = 1u };
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ uint32_t col_of(uint32_t j)
 {
     const uint32_t w = j >> 6, l = j & 63u;
@@ -243,6 +245,116 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
     return h < len ? h : len;
 }
 
+// ---------------------------------------------------------------------------
+// The whole 64-byte block loop as ONE asm statement (direct-store path).
+// hipcc's code between per-block asm statements (register copies, exec
+// bookkeeping, address math: ~40 instructions per block) cost ~6 % of the
+// loop; here a block costs 4 loads + 4 stores + 9 scalar/vector ops.
+//   * payload blocks ping-pong between two PINNED register tuples,
+//     A = v40..v55 and B = v56..v71, so the dwordx4 loads/stores and the
+//     per-byte SDWA xors name the same registers;
+//   * the next block is prefetched under an exec mask of the lanes that have
+//     one; one s_waitcnt vmcnt(8) per block (in-order VMEM completion: the
+//     8 younger ops are the previous block's stores and this prefetch);
+//   * exec shrinks as lanes run out of blocks (ragged batches), and is
+//     restored on exit.  Lanes keep their own pointer and RC4 state.
+// On entry A holds block 0 (landed), nblk >= 1 for every active lane.
+// ---------------------------------------------------------------------------
+#define ZL_XOR(R, SEL, K)                                                                        \
+    "v_xor_b32_sdwa " #R ", " #R ", %[" #K "] dst_sel:" #SEL                                     \
+    " dst_unused:UNUSED_PRESERVE src0_sel:" #SEL " src1_sel:BYTE_0\n\t"
+#define ZL_W0(D)                                                                                 \
+    ZRC4_E ZRC4_O ZL_XOR(D, BYTE_0, k0) ZRC4_E ZL_XOR(D, BYTE_1, k1)                            \
+    ZRC4_O ZL_XOR(D, BYTE_2, k0)
+#define ZL_W(DP, D)                                                                              \
+    ZRC4_E ZL_XOR(DP, BYTE_3, k1) ZRC4_O ZL_XOR(D, BYTE_0, k0)                                  \
+    ZRC4_E ZL_XOR(D, BYTE_1, k1) ZRC4_O ZL_XOR(D, BYTE_2, k0)
+#define ZL_BLOCK(d0, d1, d2, d3, d4, d5, d6, d7, d8, d9, d10, d11, d12, d13, d14, d15)            \
+    ZL_W0(d0) ZL_W(d0, d1) ZL_W(d1, d2) ZL_W(d2, d3) ZL_W(d3, d4) ZL_W(d4, d5)                  \
+    ZL_W(d5, d6) ZL_W(d6, d7) ZL_W(d7, d8) ZL_W(d8, d9) ZL_W(d9, d10) ZL_W(d10, d11)            \
+    ZL_W(d11, d12) ZL_W(d12, d13) ZL_W(d13, d14) ZL_W(d14, d15)                                 \
+    "s_waitcnt lgkmcnt(0)\n\t" ZL_XOR(d15, BYTE_3, k1)
+// payload tuples: A = v40..v55, B = v56..v71
+#define ZL_A0 "v[40:43]"
+#define ZL_A1 "v[44:47]"
+#define ZL_A2 "v[48:51]"
+#define ZL_A3 "v[52:55]"
+#define ZL_B0 "v[56:59]"
+#define ZL_B1 "v[60:63]"
+#define ZL_B2 "v[64:67]"
+#define ZL_B3 "v[68:71]"
+#define ZL_HALF_A                                                                                \
+    "v_cmp_lt_u32_e32 vcc, %[i], %[nblk]\n\t"                                                    \
+    "s_and_b64 exec, exec, vcc\n\t"                                                              \
+    "s_cbranch_execz ZL_DONE_%=\n\t"                                                             \
+    "s_add_u32 %[i1], %[i], 1\n\t"                                                               \
+    "v_cmp_lt_u32_e32 vcc, %[i1], %[nblk]\n\t"                                                   \
+    "s_and_saveexec_b64 %[tmp], vcc\n\t"                                                         \
+    "global_load_dwordx4 " ZL_B0 ", %[pa], off offset:64\n\t"                                    \
+    "global_load_dwordx4 " ZL_B1 ", %[pa], off offset:80\n\t"                                    \
+    "global_load_dwordx4 " ZL_B2 ", %[pa], off offset:96\n\t"                                    \
+    "global_load_dwordx4 " ZL_B3 ", %[pa], off offset:112\n\t"                                   \
+    "s_mov_b64 exec, %[tmp]\n\t"                                                                 \
+    "s_waitcnt vmcnt(8)\n\t"                                                                     \
+    ZL_BLOCK(v40, v41, v42, v43, v44, v45, v46, v47, v48, v49, v50, v51, v52, v53, v54, v55)    \
+    "global_store_dwordx4 %[pa], " ZL_A0 ", off\n\t"                                             \
+    "global_store_dwordx4 %[pa], " ZL_A1 ", off offset:16\n\t"                                   \
+    "global_store_dwordx4 %[pa], " ZL_A2 ", off offset:32\n\t"                                   \
+    "global_store_dwordx4 %[pa], " ZL_A3 ", off offset:48\n\t"                                   \
+    "v_lshl_add_u64 %[pa], %[pa], 0, 64\n\t"                                                     \
+    "s_add_u32 %[i], %[i], 1\n\t"
+#define ZL_HALF_B                                                                                \
+    "v_cmp_lt_u32_e32 vcc, %[i], %[nblk]\n\t"                                                    \
+    "s_and_b64 exec, exec, vcc\n\t"                                                              \
+    "s_cbranch_execz ZL_DONE_%=\n\t"                                                             \
+    "s_add_u32 %[i1], %[i], 1\n\t"                                                               \
+    "v_cmp_lt_u32_e32 vcc, %[i1], %[nblk]\n\t"                                                   \
+    "s_and_saveexec_b64 %[tmp], vcc\n\t"                                                         \
+    "global_load_dwordx4 " ZL_A0 ", %[pa], off offset:64\n\t"                                    \
+    "global_load_dwordx4 " ZL_A1 ", %[pa], off offset:80\n\t"                                    \
+    "global_load_dwordx4 " ZL_A2 ", %[pa], off offset:96\n\t"                                    \
+    "global_load_dwordx4 " ZL_A3 ", %[pa], off offset:112\n\t"                                   \
+    "s_mov_b64 exec, %[tmp]\n\t"                                                                 \
+    "s_waitcnt vmcnt(8)\n\t"                                                                     \
+    ZL_BLOCK(v56, v57, v58, v59, v60, v61, v62, v63, v64, v65, v66, v67, v68, v69, v70, v71)    \
+    "global_store_dwordx4 %[pa], " ZL_B0 ", off\n\t"                                             \
+    "global_store_dwordx4 %[pa], " ZL_B1 ", off offset:16\n\t"                                   \
+    "global_store_dwordx4 %[pa], " ZL_B2 ", off offset:32\n\t"                                   \
+    "global_store_dwordx4 %[pa], " ZL_B3 ", off offset:48\n\t"                                   \
+    "v_lshl_add_u64 %[pa], %[pa], 0, 64\n\t"                                                     \
+    "s_add_u32 %[i], %[i], 1\n\t"
+
+__device__ __forceinline__ void crypt_blocks_asm(Rc4Lane &st, uint4 *&p, uint32_t nblk,
+                                                 const uint4 (&A)[4])
+{
+    u32x4 a0 = {A[0].x, A[0].y, A[0].z, A[0].w}, a1 = {A[1].x, A[1].y, A[1].z, A[1].w};
+    u32x4 a2 = {A[2].x, A[2].y, A[2].z, A[2].w}, a3 = {A[3].x, A[3].y, A[3].z, A[3].w};
+    u32x4 b0, b1, b2, b3;
+    uint64_t pa = (uint64_t)(uintptr_t)p, save, tmp;
+    uint32_t i, i1, b, k0, k1, a1s;
+    asm volatile(
+        "s_mov_b64 %[save], exec\n\t"
+        "s_mov_b32 %[i], 0\n\t"
+        "ZL_LOOP_%=:\n\t"
+        ZL_HALF_A
+        ZL_HALF_B
+        "s_branch ZL_LOOP_%=\n\t"
+        "ZL_DONE_%=:\n\t"
+        "s_mov_b64 exec, %[save]\n\t"
+        : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1),
+          [a0] "+v"(st.a0), [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
+          [pa] "+v"(pa), [i] "=&s"(i), [i1] "=&s"(i1), [save] "=&s"(save), [tmp] "=&s"(tmp),
+          "+{v[40:43]}"(a0), "+{v[44:47]}"(a1), "+{v[48:51]}"(a2), "+{v[52:55]}"(a3),
+          "=&{v[56:59]}"(b0), "=&{v[60:63]}"(b1), "=&{v[64:67]}"(b2), "=&{v[68:71]}"(b3)
+        : [nblk] "v"(nblk)
+        : "memory", "vcc", "scc");
+    p = reinterpret_cast<uint4 *>((uintptr_t)pa);
+}
+
+#ifndef ZRC4_ASM_LOOP
+#define ZRC4_ASM_LOOP 1      // 0: per-block asm statements with hipcc's loop (A/B builds)
+#endif
+
 // Crypt one lane's message in place: unaligned head bytes, 64-byte blocks
 // (hand-written step; the next block's loads are issued before the current
 // block's keystream), 16-byte chunks, tail bytes.  If `pre` is set, A already
@@ -257,7 +369,10 @@ __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st, uint8_t *
 
     uint4 *p = reinterpret_cast<uint4 *>(msg);
     const uint32_t nblk = len >> 6;
-    if (nblk) {
+    if (ZRC4_ASM_LOOP && nblk) {
+        if (!pre) load64(A, p);
+        crypt_blocks_asm(st, p, nblk, A);
+    } else if (nblk) {
         // Ping-pong buffers A/B, no loop-carried copies, and the next block's
         // four loads issued unconditionally (re-reading the current block when
         // there is none) so the compiler's vmcnt waits stay counted and never
@@ -303,7 +418,6 @@ constexpr int kSmemBytes = kGroupBytes + 4 * kStageBytes;   // 80 KiB: 2 workgro
 // global-address-space views (pointers rebuilt from shuffled integers would
 // otherwise become flat accesses, which force vmcnt(0)+lgkmcnt(0) waits)
 typedef __attribute__((address_space(1))) uint8_t gu8;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) u32x4 gu32x4;
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v)
@@ -461,7 +575,7 @@ __device__ __forceinline__ void swap_halves(uint4 *lo, uint4 *hi)
 // Loads stay per lane (5.5 TB/s), one block pair ahead.
 __device__ __forceinline__ void crypt_message_lines(uint8_t *S, uint8_t *stage, Rc4Lane &st,
                                                     uint8_t *msg, uint32_t len, uint4 (&A)[4],
-                                                    bool pre, uint4 *A1pre = nullptr)
+                                                    bool pre)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t head = head_bytes(msg, len);
@@ -514,10 +628,6 @@ __device__ __forceinline__ void crypt_message_lines(uint8_t *S, uint8_t *stage, 
     };
 
     uint4 A1[4], B0[4], B1[4];
-    if (A1pre) {   // both blocks of the first pair were prefetched by the caller
-#pragma unroll
-        for (int i = 0; i < 4; ++i) A1[i] = A1pre[i];
-    }
     auto load_pair = [&](uint4 *d0, uint4 *d1, uint32_t b) {
         const uint32_t b0 = b < last ? b : last, b1 = b + 1u < last ? b + 1u : last;
         load4(d0, p + 4u * b0);
@@ -525,7 +635,7 @@ __device__ __forceinline__ void crypt_message_lines(uint8_t *S, uint8_t *stage, 
     };
     if (nblk) {
         if (!pre) load4(A, p);
-        if (!pre || !A1pre) load4(A1, p + 4u * (1u < last ? 1u : last));
+        load4(A1, p + 4u * (1u < last ? 1u : last));
     }
     auto pair = [&](uint32_t b, uint4 *x0, uint4 *x1) {
         if (b < nblk) xor64_asm_p(st, x0);
@@ -674,98 +784,6 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         if (!(ZRC4_ABLATE & 16)) lds_to_image(arena + (size_t)g * kGroupBytes, S);
     } else if (active && mylen) {
         scatter_column(arena, slot, S, col);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// crypt_persistent_kernel: the staged (whole-line store) kernel as a
-// persistent loop over whole 256-slot groups (contiguous range, group-aligned
-// first slot).  grid = min(groups, 2 per CU); workgroup w handles local groups
-// w, w + grid, ...  While group g's keystream runs, the next group's 64 KiB
-// image and lane data (len/off/xy) are prefetched into registers (prefetching
-// the first payload line too pushed the kernel past the register budget); at the hand-over each thread spills its own 16 image slices of
-// g and fills the prefetched slices of g' (4 at a time).  The state traffic of
-// every group but the first and last thereby overlaps keystream work instead
-// of arriving as synchronized fill/spill bursts between workgroup rounds.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256, 2)
-crypt_persistent_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
-                        uint32_t first_slot, uint8_t *__restrict__ payload,
-                        const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
-                        uint32_t n, uint32_t ngroups)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kSmemBytes];
-    uint8_t *S = smem;
-    uint4 *S4 = reinterpret_cast<uint4 *>(smem);
-    const uint32_t j = threadIdx.x;
-    const uint32_t col = col_of(j);
-    uint8_t *stage = smem + kGroupBytes + (j >> 6) * kStageBytes;
-    const uint32_t g0 = first_slot >> 8;
-
-    uint32_t gi = blockIdx.x;
-    if (gi >= ngroups) return;
-
-    uint4 img[16];
-    uint32_t nlen;
-    uint64_t noff;
-    uint16_t nxy;
-    auto prefetch = [&](uint32_t gl) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(arena + (size_t)(g0 + gl) * kGroupBytes);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) img[i] = src[i * 256 + j];
-        const uint32_t e = gl * kGroup + j;
-        const bool valid = e < n;
-        nlen = valid ? len[e] : 0u;
-        noff = valid ? off[e] : 0u;
-        nxy = (valid && nlen) ? xy[first_slot + e] : (uint16_t)0;
-    };
-
-    prefetch(gi);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) S4[i * 256 + j] = img[i];
-    __syncthreads();
-
-    while (true) {
-        // this group's lane data and first line, then the next group's prefetch
-        const uint32_t mylen = nlen;
-        uint8_t *msg = payload + noff;
-        const uint16_t sxy = nxy;
-        uint4 A[4];
-        const uint32_t gn = gi + gridDim.x;
-        const bool more = gn < ngroups;
-        if (more) prefetch(gn);
-
-        {
-            const uint32_t x = sxy & 255u, y = sxy >> 8;
-            Rc4Lane st;
-            st.col = col;
-            st.x0 = (((x + 1u) & 255u) << 8) | col;
-            st.a0 = S[st.x0];
-            st.ya = (y << 8) | col;
-            st.ta = col;
-            st.x1 = col;
-            crypt_message_lines(S, stage, st, msg, mylen, A, false);
-            if (mylen)
-                xy[first_slot + gi * kGroup + j] =
-                    (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
-        }
-        __syncthreads();
-        uint4 *dst = reinterpret_cast<uint4 *>(arena + (size_t)(g0 + gi) * kGroupBytes);
-#pragma unroll
-        for (int c = 0; c < 16; c += 4) {
-            uint4 v[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = S4[(c + k) * 256 + j];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) dst[(c + k) * 256 + j] = v[k];
-            if (more) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) S4[(c + k) * 256 + j] = img[c + k];
-            }
-        }
-        if (!more) break;
-        __syncthreads();
-        gi = gn;
     }
 }
 
