@@ -372,6 +372,73 @@ def host_inclusive(args):
             "pcie_bytes_per_pass": 2 * S * L, "note": "not the headline value (DESIGN.md)"}
 
 
+# ------------------------------------------------- connection-storm KSA rate
+def ksa_storm(args):
+    """a connection storm re-seeds every session at once
+    (RC4Encryption::makeSBox, rc4_encryption.h:46-72; two streams per session,
+    src/frame/session.cpp:110-111).  K launches of zrc4_ksa_range over all S
+    slots of the workload with device-resident 16-byte keys, timed with HIP
+    events over 16-launch segments; the CPU baseline is the oracle's
+    make_sbox on a bounded sample (1 thread, like the event-loop thread).
+    Reported in DESIGN.md; never the headline `value`."""
+    import torch
+    from zsummerx_amd import Context, synth
+    S, _ = CONFIG_SHAPES[args.workload]
+    dev = torch.device("cuda", 0)
+    ctx = Context(0, S)
+    keys = synth.keys(0, S).reshape(-1)
+    T = lambda a: torch.from_numpy(a).to(dev)
+    kl = T(np.full(S, 16, dtype=np.int32))
+    ko = T(np.arange(S, dtype=np.int64) * 16)
+    kd = T(keys)
+    st = torch.cuda.current_stream(dev)
+    for _ in range(args.warmup):
+        ctx.ksa_range(0, kl, ko, kd, n=S, stream=st)
+    torch.cuda.synchronize()
+    seg = []
+    done = 0
+    t0 = time.perf_counter()
+    while done < args.steps:
+        m = min(args.event_every, args.steps - done)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for _ in range(m):
+            ctx.ksa_range(0, kl, ko, kd, n=S, stream=st)
+        b.record(st)
+        seg.append((a, b, m))
+        done += m
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ctx.sync()
+    per = statistics.median(a.elapsed_time(b) / m for a, b, m in seg) * 1e-3   # s per launch
+    out = {"metric": "RC4 KSA streams/s (batched makeSBox, connection storm)",
+           "value": round(S / per, 1), "unit": "streams/s", "workload": args.workload,
+           "streams_per_launch": S, "key_bytes": 16, "kernel_us": round(per * 1e6, 3),
+           "ns_per_stream": round(per * 1e9 / S, 4), "wall_streams_per_s": round(S * args.steps / wall, 1),
+           "algorithmic_bytes_per_launch": S * (16 + 8 + 4 + STATE_BYTES // 2),
+           "note": "key + offset/len read, 258-B state written per stream; not the headline value"}
+    if args.cpu_seconds > 0:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import pyoracle  # cpu_baseline leg only
+        n = min(S, 65536)
+        ob = pyoracle.Batch(n)
+        kh = keys[: 16 * n]
+        offs = np.arange(n, dtype=np.uint64) * 16
+        lens = np.full(n, 16, dtype=np.uint32)
+        runs, t_end = [], time.perf_counter() + args.cpu_seconds
+        while len(runs) < 5 or time.perf_counter() < t_end:
+            t1 = time.perf_counter()
+            ob.make_sbox(kh, offs, lens)
+            runs.append(n / (time.perf_counter() - t1))
+            if len(runs) >= 50:
+                break
+        cpu = statistics.median(runs)
+        out["cpu_baseline"] = {"value": round(cpu, 1), "unit": "streams/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} x 16-byte keys, oracle make_sbox batch, median of {len(runs)} runs"}
+        out["speedup_vs_1_core"] = round(S / per / cpu, 1)
+    return out
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     p.add_argument("--gpus", type=int, default=1)
@@ -387,6 +454,8 @@ def parse(argv=None):
                    help="launches per HIP-event segment (kernel duration = segment time / N)")
     p.add_argument("--host-inclusive", action="store_true",
                    help="measure the PCIe-inclusive rate instead (DESIGN.md), one JSON line")
+    p.add_argument("--ksa", action="store_true",
+                   help="measure the connection-storm KSA rate instead (DESIGN.md), one JSON line")
     p.add_argument("--chunks", type=int, default=8)
     p.add_argument("--streams", type=int, default=3)
     return p.parse_args(argv)
@@ -397,6 +466,9 @@ def main(argv=None):
     ws, rank, local = dist_env()
     if args.host_inclusive:
         print(json.dumps(host_inclusive(args)), flush=True)
+        return
+    if args.ksa:
+        print(json.dumps(ksa_storm(args)), flush=True)
         return
     if ws != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE")
