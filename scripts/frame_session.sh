@@ -1,0 +1,31 @@
+#!/bin/bash
+# GPU-box session for the batched session engine:
+# wire-parity tests against the oracle peer, then the config-1 loopback
+# (example/frameStressTest analogue) at several session counts with the gfx950
+# hooks, the reference's own RC4 on the CPU (oracle/_ref) and RC4 off.
+#   usage: scripts/frame_session.sh [seconds]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+OUT=gpurun_out
+SECS="${1:-2}"
+REF=oracle/_ref/libzrc4_ref.so
+[ -f "$REF" ] || REF=oracle/liboracle.so
+
+timeout -k 10 300 python -u -m pytest tests/test_frame.py -m gpu -x -v --timeout 120 --timeout-method thread \
+    -p no:cacheprovider > $OUT/frame_tests.log 2>&1
+rc=$?; tail -3 $OUT/frame_tests.log; echo "[frame-tests] rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+
+: > $OUT/frame_loopback.jsonl
+for cfg in "2 1" "2 4" "64 1" "64 4" "512 1" "512 4" "2048 2"; do
+  set -- $cfg
+  for hooks in device "host:$REF" off; do
+    timeout -k 10 60 zsummerx_amd/bin/frame_stress --rc4 "$hooks" --sessions $1 --depth $2 \
+        --seconds $SECS --warmup 0.5 >> $OUT/frame_loopback.jsonl 2>> $OUT/frame_loopback.err
+    rc=$?
+    if [ $rc -ne 0 ]; then echo "[loopback $cfg $hooks] rc=$rc"; exit $rc; fi
+  done
+done
+cat $OUT/frame_loopback.jsonl
+echo done

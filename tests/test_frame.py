@@ -1,0 +1,281 @@
+"""Batched session engine (include/zsummerx_amd/frame.h): the RC4 hook sites
+of TcpSession (src/frame/session.cpp:110-111 seeding, :313-323 recv decrypt,
+:496-499 / :535-538 / :603-606 send encrypt) driven over real TCP sockets.
+
+Wire parity: an independent Python peer speaks the reference protocol with
+the oracle RC4 (one RC4Encryption per direction, both seeded from the same
+key, rc4_encryption.h:46-93) and proto4z framing (proto4z.h:704-748); the
+engine, running the hooks batched per event-loop iteration, must produce and
+accept exactly the reference's bytes.
+
+CPU tests run the engine with the oracle loaded as its hooks (host logic:
+batching, keystream order, framing, send-queue merging).  GPU tests run the
+product hooks (--rc4 device: one gfx950 launch per iteration over pinned
+SessionBlocks) against the same oracle peer."""
+import json
+import random
+import socket
+import struct
+import subprocess
+import threading
+
+import pytest
+
+from conftest import ROOT
+
+STRESS = __import__('pathlib').Path(__import__('os').environ.get('ZSX_STRESS', str(ROOT / 'zsummerx_amd' / 'bin' / 'frame_stress')))
+ORACLE_HOOKS = "host:" + str(ROOT / "oracle" / "liboracle.so")
+KEY = b"frame-parity-key\x00with-nul"   # NUL bytes count (makeSBox takes std::string)
+POLICY_REQ = b"<policy-file-request/>\x00"
+POLICY_RESP = (b'<cross-domain-policy><allow-access-from domain="*" to-ports="*"/>'
+               b"</cross-domain-policy>\x00")
+
+
+@pytest.fixture(scope="module")
+def stress(built):
+    from zsummerx_amd import build
+    build.build_frame()
+    assert STRESS.exists()
+    return STRESS
+
+
+def rc4(key=KEY):
+    import pyoracle
+    return pyoracle.Rc4(key)
+
+
+def packet(rng, size, tag):
+    body = bytes(rng.getrandbits(8) for _ in range(size - 8))
+    return struct.pack("<IHH", size, 0, tag & 0xFFFF) + body
+
+
+def recv_exact(s, n):
+    out = bytearray()
+    while len(out) < n:
+        b = s.recv(n - len(out))
+        if not b:
+            raise EOFError(f"peer closed after {len(out)} of {n} bytes")
+        out += b
+    return bytes(out)
+
+
+class Server:
+    """frame_stress --mode server; yields its port, returns its JSON stats."""
+
+    def __init__(self, stress, hooks, exit_after, *extra):
+        self.p = subprocess.Popen([str(stress), "--mode", "server", "--rc4", hooks, "--key-hex", KEY.hex(),
+                                   "--seconds", "60", "--warmup", "0", "--exit-after", str(exit_after), *extra],
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        line = self.p.stdout.readline()
+        if not line.startswith("PORT "):
+            self.p.kill()
+            raise RuntimeError(f"server did not start: {line!r} {self.p.stderr.read()}")
+        self.port = int(line.split()[1])
+
+    def finish(self, timeout=60):
+        out, err = self.p.communicate(timeout=timeout)
+        assert self.p.returncode == 0, err
+        return json.loads(out.strip().splitlines()[-1])
+
+
+def echo_client(port, seed, npk, results, idx):
+    """Send npk proto4z packets, RC4-encrypted with the oracle, in random
+    chunkings (splits inside headers and bodies, several packets per write);
+    read the echoes back and decrypt them with the oracle."""
+    rng = random.Random(seed)
+    wr, rd = rc4(), rc4()                      # session.cpp:110-111: same key both ways
+    plain = b"".join(packet(rng, rng.choice([8, 9, 64, 1000, 1024, 4096, 20000, rng.randint(8, 3000)]), i)
+                     for i in range(npk))
+    wire = wr.encryption(plain)
+    with socket.create_connection(("127.0.0.1", port), timeout=30) as s:
+        s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        got = bytearray()
+        pos = 0
+        while pos < len(wire):
+            n = rng.choice([1, 3, 7, 100, 1500, 9000, 40000])
+            s.sendall(wire[pos:pos + n])
+            pos += n
+            s.setblocking(False)
+            try:
+                while True:
+                    b = s.recv(1 << 16)
+                    if not b:
+                        break
+                    got += b
+            except BlockingIOError:
+                pass
+            s.setblocking(True)
+        s.settimeout(30)
+        got += recv_exact(s, len(wire) - len(got))
+    results[idx] = (plain, bytes(got), rd.encryption(bytes(got)))
+
+
+def run_echo_parity(stress, hooks, nclients=6, npk=40):
+    srv = Server(stress, hooks, nclients)
+    results = [None] * nclients
+    th = [threading.Thread(target=echo_client, args=(srv.port, 1000 + i, npk, results, i)) for i in range(nclients)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    stats = srv.finish()
+    for i, r in enumerate(results):
+        assert r is not None, f"client {i} did not finish"
+        plain, cipher, decrypted = r
+        assert len(cipher) == len(plain)
+        # the server's ciphertext is exactly RC4Encryption(key) over the echoed bytes
+        assert cipher == rc4().encryption(plain), f"client {i}: server wire bytes differ from the reference RC4"
+        assert decrypted == plain
+    assert stats["recv_packs"] == nclients * npk
+    assert stats["linked"] == nclients
+    return stats
+
+
+def run_engine_client(stress, hooks, nsess=4, echoes=25, block=1024, depth=2):
+    """The engine as the connecting side against a Python oracle server."""
+    lst = socket.socket()
+    lst.bind(("127.0.0.1", 0))
+    lst.listen(64)
+    port = lst.getsockname()[1]
+    errors = []
+
+    def serve_one(conn):
+        rd, wr = rc4(), rc4()
+        buf = b""
+        try:
+            with conn:
+                while True:
+                    b = conn.recv(1 << 16)
+                    if not b:
+                        return
+                    buf += rd.encryption(b)
+                    out = b""
+                    while len(buf) >= 6:                     # proto4z.h:704-748
+                        ln = struct.unpack_from("<I", buf)[0]
+                        if ln < 6 or ln > 20480:
+                            errors.append(f"bad length {ln}")
+                            return
+                        if len(buf) < ln:
+                            break
+                        out += buf[:ln]
+                        buf = buf[ln:]
+                    if out:
+                        conn.sendall(wr.encryption(out))
+        except (ConnectionResetError, BrokenPipeError):
+            return      # the engine closes after its last echo with packets still in flight (depth > 1)
+        except Exception as e:                                # noqa: BLE001
+            errors.append(repr(e))
+
+    def acceptor():
+        for _ in range(nsess):
+            c, _ = lst.accept()
+            threading.Thread(target=serve_one, args=(c,), daemon=True).start()
+
+    threading.Thread(target=acceptor, daemon=True).start()
+    p = subprocess.run([str(stress), "--mode", "client", "--port", str(port), "--rc4", hooks,
+                        "--key-hex", KEY.hex(), "--sessions", str(nsess), "--echoes", str(echoes),
+                        "--block", str(block), "--depth", str(depth), "--seconds", "60", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=120)
+    lst.close()
+    assert p.returncode == 0, p.stderr
+    st = json.loads(p.stdout.strip().splitlines()[-1])
+    assert not errors, errors
+    assert st["mismatches"] == 0
+    assert st["echoes"] == nsess * echoes
+    return st
+
+
+def run_flash_policy(stress, hooks):
+    """session.cpp:290-311: the probe is matched on the raw bytes (not
+    decrypted), the answer goes out through send() -- i.e. encrypted -- and the
+    read stream is untouched, so the next packet decrypts from offset 0."""
+    srv = Server(stress, hooks, 1, "--flash-policy")
+    wr, rd = rc4(), rc4()
+    with socket.create_connection(("127.0.0.1", srv.port), timeout=30) as s:
+        s.sendall(POLICY_REQ)
+        resp = recv_exact(s, len(POLICY_RESP))
+        assert rd.encryption(resp) == POLICY_RESP
+        pk = packet(random.Random(5), 300, 1)
+        s.sendall(wr.encryption(pk))
+        assert rd.encryption(recv_exact(s, len(pk))) == pk
+    srv.finish()
+
+
+def run_corrupt_closes(stress, hooks):
+    """A length field below the 6-byte header is BCT_CORRUPTION: the session is
+    closed (session.cpp:355-361), the peer sees EOF."""
+    srv = Server(stress, hooks, 1)
+    wr = rc4()
+    with socket.create_connection(("127.0.0.1", srv.port), timeout=30) as s:
+        s.sendall(wr.encryption(struct.pack("<IHH", 3, 0, 0)))
+        assert s.recv(100) == b""
+    st = srv.finish()
+    assert st["closed"] == 1
+
+
+# ------------------------------------------------------------------ CPU
+def test_engine_echo_parity_cpu_hooks(stress):
+    run_echo_parity(stress, ORACLE_HOOKS)
+
+
+def test_engine_as_client_cpu_hooks(stress):
+    run_engine_client(stress, ORACLE_HOOKS)
+
+
+def test_flash_policy_cpu_hooks(stress):
+    run_flash_policy(stress, ORACLE_HOOKS)
+
+
+def test_corrupt_packet_closes_cpu_hooks(stress):
+    run_corrupt_closes(stress, ORACLE_HOOKS)
+
+
+def test_loopback_cpu_hooks(stress):
+    p = subprocess.run([str(stress), "--rc4", ORACLE_HOOKS, "--sessions", "16", "--depth", "3",
+                        "--seconds", "0.5", "--warmup", "0.1"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    st = json.loads(p.stdout)
+    assert st["mismatches"] == 0 and st["echoes"] > 0 and st["linked"] == 32
+    assert st["spans_per_call"] > 1.0          # hooks really are batched
+
+
+def test_no_device_is_loud(stress):
+    import torch  # noqa: F401  (only to know whether a GPU exists here)
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    p = subprocess.run([str(stress), "--rc4", "device", "--seconds", "0.1"], capture_output=True, text=True,
+                       timeout=60)
+    assert p.returncode == 1 and "gfx950" in p.stderr
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+def test_engine_echo_parity_device(stress):
+    st = run_echo_parity(stress, "device")
+    assert st["rc4"] == "zrc4-gfx950"
+
+
+@pytest.mark.gpu
+def test_engine_as_client_device(stress):
+    st = run_engine_client(stress, "device", nsess=8, echoes=40, block=2000, depth=3)
+    assert st["rc4"] == "zrc4-gfx950"
+
+
+@pytest.mark.gpu
+def test_flash_policy_device(stress):
+    run_flash_policy(stress, "device")
+
+
+@pytest.mark.gpu
+def test_corrupt_packet_closes_device(stress):
+    run_corrupt_closes(stress, "device")
+
+
+@pytest.mark.gpu
+def test_loopback_device(stress):
+    p = subprocess.run([str(stress), "--rc4", "device", "--sessions", "64", "--depth", "4",
+                        "--seconds", "1", "--warmup", "0.2"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    st = json.loads(p.stdout)
+    assert st["rc4"] == "zrc4-gfx950"
+    assert st["mismatches"] == 0 and st["echoes"] > 0 and st["linked"] == 128

@@ -3,6 +3,9 @@ the GPU box with the repo snapshot).
 
   libzrc4.so        C-ABI product library: HIP kernels for gfx950 + host side
   libzrc4_synth.so  synthetic workload generator (bench/tests input data)
+  libzsx_frame.so   batched session engine (include/zsummerx_amd/frame.h) with
+                    the gfx950 RC4 hooks over libzrc4.so
+  bin/frame_stress  BASELINE config-1 driver (example/frameStressTest analogue)
   oracle/           CPU restatement (+ oracle/_ref when /root/reference exists)
 """
 from __future__ import annotations
@@ -20,6 +23,14 @@ ARCH = "gfx950"
 
 LIB = PKG / "libzrc4.so"
 SYNTH = PKG / "libzrc4_synth.so"
+
+FRAME = PKG / "libzsx_frame.so"
+STRESS = PKG / "bin" / "frame_stress"
+ENGINE = PKG / "engine"
+FRAME_SOURCES = [ENGINE / "frame.cpp", ENGINE / "rc4_hooks_device.cpp"]
+FRAME_DEPS = FRAME_SOURCES + [ROOT / "include" / "zsummerx_amd" / "frame.h",
+                              ROOT / "include" / "zsummerx_amd" / "rc4_hooks.h", ROOT / "include" / "zrc4.h"]
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
 HIP_SOURCES = [CSRC / "zrc4.hip"]
 HIP_DEPS = HIP_SOURCES + [CSRC / "zrc4_kernels.hpp", ROOT / "include" / "zrc4.h"]
@@ -85,6 +96,28 @@ def build_synth(force: bool = False) -> Path:
     return SYNTH
 
 
+def build_frame(force: bool = False) -> Path:
+    """The session engine: host C++ (g++) against the HIP runtime API and the
+    C-ABI of libzrc4.so; the stress driver links it (rpath $ORIGIN)."""
+    lib = build_lib(force)
+    if force or _stale(FRAME, FRAME_DEPS + [lib]):
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-Wno-unused-parameter",
+               "-D__HIP_PLATFORM_AMD__", f"-I{ROOT / 'include'}", f"-I{ROCM / 'include'}",
+               "-o", str(FRAME), *map(str, FRAME_SOURCES),
+               f"-L{PKG}", "-lzrc4", f"-L{ROCM / 'lib'}", "-lamdhip64",
+               "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{ROCM / 'lib'}"]
+        subprocess.run(cmd, check=True)
+    src = ROOT / "tools" / "frame_stress.cpp"
+    if force or _stale(STRESS, [src, FRAME] + FRAME_DEPS):
+        STRESS.parent.mkdir(exist_ok=True)
+        cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter",
+               f"-I{ROOT / 'include'}", "-o", str(STRESS), str(src),
+               f"-L{PKG}", "-lzsx_frame", "-lzrc4", "-ldl",
+               "-Wl,-rpath,$ORIGIN/..", f"-Wl,-rpath,{ROCM / 'lib'}"]
+        subprocess.run(cmd, check=True)
+    return FRAME
+
+
 def build_oracle() -> None:
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
 
@@ -92,6 +125,7 @@ def build_oracle() -> None:
 def build_all(force: bool = False) -> None:
     build_lib(force)
     build_synth(force)
+    build_frame(force)
     build_oracle()
 
 

@@ -18,6 +18,7 @@ struct zrc4_ctx {
     uint8_t *arena;         // capacity/256 groups x 64 KiB S-box images
     uint16_t *xy;           // per slot: x | y << 8
     uint32_t *err;          // latched device-side fault bits
+    uint32_t *h_err;        // pinned read-back word for err
     // staging for the *_host entry points (grown on demand)
     uint8_t *d_stage;
     size_t d_stage_bytes;
@@ -93,12 +94,15 @@ int launch_ksa(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, const uint
     return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
 }
 
+// One stream-ordered read-back into pinned memory and ONE wait: this is the
+// per-iteration completion point of the session engine's hooks, so it must not
+// cost more than the wait itself.
 int check_err(zrc4_ctx *c, hipStream_t s)
 {
-    uint32_t h = 0;
-    ZRC4_TRY(hipMemcpyAsync(&h, c->err, sizeof(h), hipMemcpyDeviceToHost, s));
+    *c->h_err = 0;
+    ZRC4_TRY(hipMemcpyAsync(c->h_err, c->err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     ZRC4_TRY(hipStreamSynchronize(s));
-    if (h) {
+    if (*c->h_err) {
         ZRC4_TRY(hipMemsetAsync(c->err, 0, sizeof(uint32_t), s));
         ZRC4_TRY(hipStreamSynchronize(s));
         return ZRC4_ERR_SLOT_RANGE;
@@ -133,6 +137,7 @@ int zrc4_create(zrc4_ctx **out, int device, uint32_t capacity)
     bool ok = hipMalloc(&c->arena, groups * (size_t)zrc4::kGroupBytes) == hipSuccess &&
               hipMalloc(&c->xy, (size_t)c->capacity * sizeof(uint16_t)) == hipSuccess &&
               hipMalloc(&c->err, sizeof(uint32_t)) == hipSuccess &&
+              hipHostMalloc(&c->h_err, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
               hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     if (!ok) { zrc4_destroy(c); return ZRC4_ERR_OUT_OF_MEMORY; }
     // Fresh slots hold the reference's empty-key state: identity box, x = y = 0
@@ -158,6 +163,7 @@ int zrc4_destroy(zrc4_ctx *c)
     if (c->arena) (void)hipFree(c->arena);
     if (c->xy) (void)hipFree(c->xy);
     if (c->err) (void)hipFree(c->err);
+    if (c->h_err) (void)hipHostFree(c->h_err);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -212,7 +218,6 @@ int zrc4_sync(zrc4_ctx *c, void *stream)
     if (!c) return ZRC4_ERR_INVALID_ARG;
     int rc = set_device(c);
     if (rc) return rc;
-    ZRC4_TRY(hipStreamSynchronize((hipStream_t)stream));
     return check_err(c, (hipStream_t)stream);
 }
 
