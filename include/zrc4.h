@@ -114,6 +114,21 @@ int zrc4_make_sbox(zrc4_ctx *ctx, uint32_t id, const uint8_t *key,
                    size_t keylen);
 int zrc4_encryption(zrc4_ctx *ctx, uint32_t id, uint8_t *data, int length);
 
+/* Keystream reservoirs (the session engine's low-latency hook path,
+ * zsummerx_amd/engine/rc4_hooks_device.cpp).  RC4's keystream does not depend
+ * on the data, so a slot's keystream can be generated ahead into a device
+ * ring of ring_cap bytes (ring r at ring + r * ring_cap) by zrc4_crypt over
+ * ZEROED ring bytes (0 ^ k = k; the slot's state advances as usual).
+ * zrc4_xor_ring then XORs entry i's payload[off[i] .. off[i]+len[i]) with
+ * ring rid[i] from position pos[i] on (wrapping mod ring_cap) and zeroes the
+ * ring bytes it used.  Requires len[i] <= ring_cap and pos[i] < ring_cap; the
+ * caller tracks which ring bytes hold keystream.  Device (or pinned host)
+ * pointers; asynchronous on `stream`.  Touches no slot state. */
+int zrc4_xor_ring(zrc4_ctx *ctx, uint8_t *ring, uint32_t ring_cap,
+                  const uint32_t *rid, const uint32_t *pos, uint8_t *payload,
+                  const uint64_t *off, const uint32_t *len, uint32_t n,
+                  void *stream);
+
 /* Wait for `stream`, then report (and clear) any latched device-side fault. */
 int zrc4_sync(zrc4_ctx *ctx, void *stream);
 

@@ -51,8 +51,11 @@ public:
 };
 
 // The gfx950 implementation over libzrc4.so (throws std::runtime_error when no
-// usable device exists or the context cannot be created).
-std::unique_ptr<Rc4Hooks> makeDeviceRc4Hooks(int device, uint32_t capacity);
+// usable device exists or the context cannot be created).  ringBytes > 0
+// selects the keystream-reservoir mode (per-slot device rings of that many
+// bytes, >= SESSION_BLOCK_SIZE; see rc4_hooks_device.cpp), 0 the direct mode
+// (one zrc4_crypt over the spans per iteration).
+std::unique_ptr<Rc4Hooks> makeDeviceRc4Hooks(int device, uint32_t capacity, uint32_t ringBytes = 32768);
 
 // Hooks for an engine whose sessions all have RC4 off (empty
 // _rc4TcpEncryption): plain host blocks; seed()/crypt() fail with

@@ -12,20 +12,29 @@ SECS="${1:-2}"
 REF=oracle/_ref/libzrc4_ref.so
 [ -f "$REF" ] || REF=oracle/liboracle.so
 
-timeout -k 10 300 python -u -m pytest tests/test_frame.py -m gpu -x -v --timeout 120 --timeout-method thread \
-    -p no:cacheprovider > $OUT/frame_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_frame.py tests/test_hooks.py -m gpu -x -v --timeout 120 \
+    --timeout-method thread -p no:cacheprovider > $OUT/frame_tests.log 2>&1
 rc=$?; tail -3 $OUT/frame_tests.log; echo "[frame-tests] rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 
 : > $OUT/frame_loopback.jsonl
 for cfg in "2 1" "2 4" "64 1" "64 4" "512 1" "512 4" "2048 2"; do
   set -- $cfg
-  for hooks in device "host:$REF" off; do
+  for hooks in device device-direct "host:$REF" off; do
     timeout -k 10 60 zsummerx_amd/bin/frame_stress --rc4 "$hooks" --sessions $1 --depth $2 \
         --seconds $SECS --warmup 0.5 >> $OUT/frame_loopback.jsonl 2>> $OUT/frame_loopback.err
     rc=$?
     if [ $rc -ne 0 ]; then echo "[loopback $cfg $hooks] rc=$rc"; exit $rc; fi
   done
 done
-cat $OUT/frame_loopback.jsonl
+timeout -k 10 60 tools/bin/hostmem_probe 2 1024 200 > $OUT/hostmem_probe.jsonl 2>&1 || exit $?
+python3 - <<'PY'
+import json
+print("%-20s %8s %6s %12s %10s %8s" % ("hooks", "sessions", "depth", "echo/s", "us/call", "spans"))
+for l in open("gpurun_out/frame_loopback.jsonl"):
+    d = json.loads(l)
+    print("%-20s %8d %6d %12.0f %10.1f %8.1f %s" % (d["rc4"], d["sessions"], d["depth"], d["echo_per_s"],
+          d["rc4_us_per_call"], d["spans_per_call"], "" if d["mismatches"] == 0 else "MISMATCH"))
+PY
+head -8 $OUT/hostmem_probe.jsonl
 echo done

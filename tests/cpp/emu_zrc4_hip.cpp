@@ -1,0 +1,130 @@
+// emu_zrc4_hip.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// A CPU emulation of exactly the surface zsummerx_amd/engine/rc4_hooks_device.cpp
+// uses -- the zrc4 C-ABI (include/zrc4.h) and a handful of HIP runtime calls --
+// so the device hooks' HOST logic (reservoir levels, ring positions, top-up
+// pieces, refill commits, reseeding) can be exercised on a machine without a
+// GPU.  Every "launch" runs synchronously on the CPU; RC4 is the oracle
+// restatement (oracle/rc4_oracle.c, pinned to rc4_encryption.h:46-93).  It is
+// linked only into tests' emulated frame_stress binary (tests/test_frame.py),
+// never into the product library.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "zrc4.h"
+extern "C" {
+#include "rc4_oracle.h"
+}
+
+struct zrc4_ctx {
+    std::vector<oracle_rc4_state> st;
+};
+
+extern "C" {
+
+int zrc4_create(zrc4_ctx **out, int, uint32_t capacity)
+{
+    auto *c = new zrc4_ctx();
+    c->st.resize((capacity + 255u) & ~255u);
+    for (auto &s : c->st) oracle_make_sbox(&s, nullptr, 0);
+    *out = c;
+    return ZRC4_OK;
+}
+int zrc4_destroy(zrc4_ctx *c)
+{
+    delete c;
+    return ZRC4_OK;
+}
+uint32_t zrc4_capacity(const zrc4_ctx *c) { return (uint32_t)c->st.size(); }
+int zrc4_ksa(zrc4_ctx *c, const uint32_t *ids, const uint8_t *keys, const uint64_t *ko, const uint32_t *kl,
+             uint32_t n, void *)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t s = ids ? ids[i] : i;
+        if (s >= c->st.size()) return ZRC4_ERR_SLOT_RANGE;
+        oracle_make_sbox(&c->st[s], keys + ko[i], kl[i]);
+    }
+    return ZRC4_OK;
+}
+int zrc4_crypt(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_t *off, const uint32_t *len,
+               uint32_t n, void *)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t s = ids ? ids[i] : i;
+        if (s >= c->st.size()) return ZRC4_ERR_SLOT_RANGE;
+        oracle_encryption(&c->st[s], payload + off[i], (long)len[i]);
+    }
+    return ZRC4_OK;
+}
+int zrc4_xor_ring(zrc4_ctx *, uint8_t *ring, uint32_t cap, const uint32_t *rid, const uint32_t *pos,
+                  uint8_t *payload, const uint64_t *off, const uint32_t *len, uint32_t n, void *)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t *r = ring + (size_t)rid[i] * cap;
+        uint8_t *d = payload + off[i];
+        for (uint32_t k = 0; k < len[i]; ++k) {
+            uint32_t q = pos[i] + k;
+            if (q >= cap) q -= cap;
+            d[k] ^= r[q];
+            r[q] = 0;
+        }
+    }
+    return ZRC4_OK;
+}
+int zrc4_sync(zrc4_ctx *, void *) { return ZRC4_OK; }
+const char *zrc4_strerror(int) { return "emulated zrc4"; }
+
+}  // extern "C"
+
+// HIP runtime calls used by the hooks (C++ linkage, as hip_runtime_api.h declares them).
+hipError_t hipSetDevice(int) { return hipSuccess; }
+hipError_t hipHostMalloc(void **p, size_t n, unsigned int)
+{
+    *p = std::aligned_alloc(64, (n + 63) / 64 * 64);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipHostFree(void *p)
+{
+    std::free(p);
+    return hipSuccess;
+}
+hipError_t hipMalloc(void **p, size_t n)
+{
+    *p = std::aligned_alloc(64, (n + 63) / 64 * 64);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipFree(void *p)
+{
+    std::free(p);
+    return hipSuccess;
+}
+hipError_t hipMemsetAsync(void *p, int v, size_t n, hipStream_t)
+{
+    std::memset(p, v, n);
+    return hipSuccess;
+}
+static int g_stream_tag;
+hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned int)
+{
+    *s = reinterpret_cast<hipStream_t>(&g_stream_tag);
+    return hipSuccess;
+}
+hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
+static int g_event_tag;
+hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned)
+{
+    *e = reinterpret_cast<hipEvent_t>(&g_event_tag);
+    return hipSuccess;
+}
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+// Alternate "not ready" / "done" so both commit paths (poll and wait) run.
+hipError_t hipEventQuery(hipEvent_t)
+{
+    static unsigned k;
+    return (++k % 3) ? hipErrorNotReady : hipSuccess;
+}
+hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }

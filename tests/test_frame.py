@@ -118,9 +118,13 @@ def run_echo_parity(stress, hooks, nclients=6, npk=40):
         t.start()
     for t in th:
         t.join(120)
+    if any(r is None for r in results):
+        srv.p.kill()
+        _, err = srv.p.communicate(timeout=30)
+        raise AssertionError(f"clients {[i for i, r in enumerate(results) if r is None]} did not finish; "
+                             f"server stderr: {err[-3000:]}")
     stats = srv.finish()
     for i, r in enumerate(results):
-        assert r is not None, f"client {i} did not finish"
         plain, cipher, decrypted = r
         assert len(cipher) == len(plain)
         # the server's ciphertext is exactly RC4Encryption(key) over the echoed bytes
@@ -214,6 +218,24 @@ def run_corrupt_closes(stress, hooks):
 
 
 # ------------------------------------------------------------------ CPU
+@pytest.fixture(scope="module")
+def stress_emu(built):
+    """The engine with the DEVICE hooks' host logic (keystream reservoirs) over a
+    CPU emulation of the zrc4 C-ABI (tests/cpp/emu_zrc4_hip.cpp)."""
+    from zsummerx_amd import build
+    build.build_test_tools()
+    return ROOT / "tools" / "bin" / "frame_stress_emu"
+
+
+def test_engine_echo_parity_emulated_device_hooks(stress_emu):
+    st = run_echo_parity(stress_emu, "device")
+    assert st["rc4"] == "zrc4-gfx950"
+
+
+def test_engine_as_client_emulated_device_hooks(stress_emu):
+    run_engine_client(stress_emu, "device", nsess=6, echoes=30, block=3000, depth=3)
+
+
 def test_engine_echo_parity_cpu_hooks(stress):
     run_echo_parity(stress, ORACLE_HOOKS)
 

@@ -1,0 +1,56 @@
+"""The device Rc4Hooks (zsummerx_amd/engine/rc4_hooks_device.cpp) driven with
+the session engine's call pattern -- seeding both streams per session, rounds
+of crypt() over ragged spans inside pooled SessionBlocks, reconnect reseeds --
+every byte checked against the oracle RC4 (rc4_encryption.h:46-93) by
+tests/cpp/hooks_check.cpp.
+
+CPU: the hooks' host logic (keystream-reservoir levels, ring wrap, two-piece
+top-ups, refill commits, reseed drains) over a CPU emulation of the zrc4
+C-ABI (tests/cpp/emu_zrc4_hip.cpp).  GPU: the real gfx950 path, reservoir and
+direct modes."""
+import json
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+BIN = ROOT / "tools" / "bin"
+
+
+@pytest.fixture(scope="module")
+def tools(built):
+    from zsummerx_amd import build
+    build.build_test_tools()
+    return BIN
+
+
+def run(exe, *args, env=None):
+    p = subprocess.run([str(exe), *map(str, args)], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, (p.stdout, p.stderr)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["ok"], out
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_reservoir_host_logic_emulated(tools, seed):
+    run(tools / "hooks_check_emu", "device", 48, 150, seed)
+
+
+def test_direct_host_logic_emulated(tools):
+    run(tools / "hooks_check_emu", "direct", 16, 40, 9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,sessions,rounds,seed", [("device", 64, 300, 1), ("device", 300, 100, 7),
+                                                        ("direct", 64, 80, 2)])
+def test_device_hooks_vs_oracle(tools, mode, sessions, rounds, seed):
+    run(tools / "hooks_check", mode, sessions, rounds, seed)
+
+
+@pytest.mark.gpu
+def test_device_hooks_synchronous_refill(tools):
+    import os
+    env = dict(os.environ, ZSX_RESERVOIR_SYNC_REFILL="1")
+    run(tools / "hooks_check", "device", 64, 120, 4, env=env)

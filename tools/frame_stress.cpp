@@ -10,7 +10,9 @@
 //
 // Modes: loopback (server + clients in ONE engine / event loop, the default),
 // server (prints "PORT <n>", serves until --seconds or --exit-after closes),
-// client (--port P).  RC4 hooks: --rc4 device (the gfx950 product path) |
+// client (--port P).  RC4 hooks: --rc4 device (the gfx950 product path,
+// keystream reservoirs of --ring bytes per stream) | device-direct (one crypt
+// launch over the spans per iteration) |
 // host:<lib> (a CPU RC4Encryption loaded from <lib> -- oracle/liboracle.so or
 // oracle/_ref/libzrc4_ref.so; tests and the CPU baseline only) | off.
 // Prints one JSON line of counters.
@@ -109,6 +111,7 @@ struct Args {
     unsigned echoes = 0;          // client: close a session after this many echoes (0 = run by time)
     bool flashPolicy = false;
     int device = 0;
+    unsigned ring = 32768;        // keystream reservoir bytes per slot (device hooks)
 };
 
 double now()
@@ -175,6 +178,7 @@ static int run(int argc, char **argv)
         else if (k == "--echoes") a.echoes = (unsigned)std::stoul(val());
         else if (k == "--flash-policy") a.flashPolicy = true;
         else if (k == "--device") a.device = std::stoi(val());
+        else if (k == "--ring") a.ring = (unsigned)std::stoul(val());
         else {
             std::fprintf(stderr, "unknown option %s\n", k.c_str());
             return 2;
@@ -188,11 +192,12 @@ static int run(int argc, char **argv)
 
     SessionManager mgr;
     const uint32_t slots = 2u * (2u * a.sessions + 1024u);   // both sides + accepted extras
-    if (a.rc4 == "device") mgr.setRc4Hooks(makeDeviceRc4Hooks(a.device, slots));
+    if (a.rc4 == "device") mgr.setRc4Hooks(makeDeviceRc4Hooks(a.device, slots, a.ring));
+    else if (a.rc4 == "device-direct") mgr.setRc4Hooks(makeDeviceRc4Hooks(a.device, slots, 0));
     else if (a.rc4.rfind("host:", 0) == 0) mgr.setRc4Hooks(std::unique_ptr<Rc4Hooks>(new HostLibHooks(a.rc4.substr(5), slots)));
     else if (a.rc4 == "off") mgr.setRc4Hooks(makeKeylessHooks());
     else {
-        std::fprintf(stderr, "--rc4 must be device, host:<lib> or off\n");
+        std::fprintf(stderr, "--rc4 must be device, device-direct, host:<lib> or off\n");
         return 2;
     }
     mgr.start();

@@ -98,6 +98,12 @@ class Context:
         check(self._lib.zrc4_crypt_range(self._h, int(first_slot), _ptr(payload), _ptr(off),
                                          _ptr(length), n, _stream(stream)), "zrc4_crypt_range")
 
+    def xor_ring(self, ring, ring_cap: int, rid, pos, payload, off, length, n=None, stream=None) -> None:
+        """zrc4_xor_ring: payload spans ^= keystream rings (consumed bytes zeroed)."""
+        n = int(length.numel() if n is None else n)
+        check(self._lib.zrc4_xor_ring(self._h, _ptr(ring), int(ring_cap), _ptr(rid), _ptr(pos), _ptr(payload),
+                                      _ptr(off), _ptr(length), n, _stream(stream)), "zrc4_xor_ring")
+
     def sync(self, stream=None) -> None:
         check(self._lib.zrc4_sync(self._h, _stream(stream)), "zrc4_sync")
 

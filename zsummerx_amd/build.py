@@ -118,6 +118,40 @@ def build_frame(force: bool = False) -> Path:
     return FRAME
 
 
+def build_test_tools(force: bool = False) -> None:
+    """Test infrastructure (links the oracle; never part of the product):
+      tools/bin/hooks_check      the device Rc4Hooks driven like the engine,
+                                 every byte checked against the oracle (GPU)
+      tools/bin/hooks_check_emu  the same host logic over a CPU emulation of
+                                 the zrc4 C-ABI (tests/cpp/emu_zrc4_hip.cpp)
+      tools/bin/frame_stress_emu the engine + device hooks over that emulation"""
+    frame = build_frame(force)
+    out = ROOT / "tools" / "bin"
+    out.mkdir(parents=True, exist_ok=True)
+    orc = ROOT / "oracle" / "liboracle.so"
+    chk = ROOT / "tests" / "cpp" / "hooks_check.cpp"
+    emu = ROOT / "tests" / "cpp" / "emu_zrc4_hip.cpp"
+    dev = ENGINE / "rc4_hooks_device.cpp"
+    common = ["-std=c++17", f"-I{ROOT / 'include'}", f"-I{ROOT / 'oracle'}"]
+    emu_flags = ["-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}"]
+    oracle_link = [f"-L{ROOT / 'oracle'}", "-loracle", "-Wl,-rpath,$ORIGIN/../../oracle"]
+    jobs = [
+        (out / "hooks_check", [chk, orc, frame] + FRAME_DEPS,
+         ["g++", "-O2", *common, "-o", str(out / "hooks_check"), str(chk), *oracle_link,
+          f"-L{PKG}", "-lzsx_frame", "-lzrc4", "-lpthread", "-Wl,-rpath,$ORIGIN/../../zsummerx_amd",
+          f"-Wl,-rpath,{ROCM / 'lib'}"]),
+        (out / "hooks_check_emu", [chk, orc, emu] + FRAME_DEPS,
+         ["g++", "-O2", *common, *emu_flags, "-o", str(out / "hooks_check_emu"), str(chk), str(dev), str(emu),
+          *oracle_link, "-lpthread"]),
+        (out / "frame_stress_emu", [orc, emu, ROOT / "tools" / "frame_stress.cpp"] + FRAME_DEPS,
+         ["g++", "-O2", *common, *emu_flags, "-o", str(out / "frame_stress_emu"), str(ROOT / "tools" / "frame_stress.cpp"),
+          *map(str, FRAME_SOURCES), str(emu), *oracle_link, "-ldl", "-lpthread"]),
+    ]
+    for target, deps, cmd in jobs:
+        if force or _stale(target, deps):
+            subprocess.run(cmd, check=True)
+
+
 def build_oracle() -> None:
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
 
@@ -127,6 +161,7 @@ def build_all(force: bool = False) -> None:
     build_synth(force)
     build_frame(force)
     build_oracle()
+    build_test_tools(force)
 
 
 if __name__ == "__main__":

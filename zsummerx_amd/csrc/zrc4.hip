@@ -17,8 +17,9 @@ struct zrc4_ctx {
     uint32_t capacity;      // multiple of 256
     uint8_t *arena;         // capacity/256 groups x 64 KiB S-box images
     uint16_t *xy;           // per slot: x | y << 8
-    uint32_t *err;          // latched device-side fault bits
-    uint32_t *h_err;        // pinned read-back word for err
+    uint32_t *err;          // latched device-side fault bits, in pinned host memory:
+                            // kernels latch with a plain store, the host reads it
+                            // after the stream wait (no read-back copy)
     // staging for the *_host entry points (grown on demand)
     uint8_t *d_stage;
     size_t d_stage_bytes;
@@ -94,17 +95,15 @@ int launch_ksa(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, const uint
     return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
 }
 
-// One stream-ordered read-back into pinned memory and ONE wait: this is the
-// per-iteration completion point of the session engine's hooks, so it must not
-// cost more than the wait itself.
+// The per-iteration completion point of the session engine's hooks: ONE
+// stream wait, then the latch word is read straight from pinned memory (a
+// device-to-host copy of it used to cost another ~11 us per call).
 int check_err(zrc4_ctx *c, hipStream_t s)
 {
-    *c->h_err = 0;
-    ZRC4_TRY(hipMemcpyAsync(c->h_err, c->err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     ZRC4_TRY(hipStreamSynchronize(s));
-    if (*c->h_err) {
-        ZRC4_TRY(hipMemsetAsync(c->err, 0, sizeof(uint32_t), s));
-        ZRC4_TRY(hipStreamSynchronize(s));
+    volatile uint32_t *e = c->err;
+    if (*e) {
+        *e = 0u;
         return ZRC4_ERR_SLOT_RANGE;
     }
     return ZRC4_OK;
@@ -136,17 +135,16 @@ int zrc4_create(zrc4_ctx **out, int device, uint32_t capacity)
     const size_t groups = c->capacity / zrc4::kGroup;
     bool ok = hipMalloc(&c->arena, groups * (size_t)zrc4::kGroupBytes) == hipSuccess &&
               hipMalloc(&c->xy, (size_t)c->capacity * sizeof(uint16_t)) == hipSuccess &&
-              hipMalloc(&c->err, sizeof(uint32_t)) == hipSuccess &&
-              hipHostMalloc(&c->h_err, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc(&c->err, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
               hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     if (!ok) { zrc4_destroy(c); return ZRC4_ERR_OUT_OF_MEMORY; }
     // Fresh slots hold the reference's empty-key state: identity box, x = y = 0
     // (what makeSBox("") produces, rc4_encryption.h:48-53).
+    *c->err = 0u;
     hipLaunchKernelGGL(zrc4::identity_kernel, dim3((unsigned)groups), dim3(zrc4::kGroup), 0,
                        c->stream, c->arena);
     if (hipGetLastError() != hipSuccess ||
         hipMemsetAsync(c->xy, 0, (size_t)c->capacity * sizeof(uint16_t), c->stream) != hipSuccess ||
-        hipMemsetAsync(c->err, 0, sizeof(uint32_t), c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         zrc4_destroy(c);
         return ZRC4_ERR_HIP;
@@ -162,8 +160,7 @@ int zrc4_destroy(zrc4_ctx *c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->arena) (void)hipFree(c->arena);
     if (c->xy) (void)hipFree(c->xy);
-    if (c->err) (void)hipFree(c->err);
-    if (c->h_err) (void)hipHostFree(c->h_err);
+    if (c->err) (void)hipHostFree(c->err);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -211,6 +208,20 @@ int zrc4_crypt_range(zrc4_ctx *c, uint32_t first_slot, uint8_t *payload, const u
     int rc = set_device(c);
     if (rc) return rc;
     return launch_crypt(c, nullptr, first_slot, payload, off, len, n, (hipStream_t)stream);
+}
+
+int zrc4_xor_ring(zrc4_ctx *c, uint8_t *ring, uint32_t ring_cap, const uint32_t *rid,
+                  const uint32_t *pos, uint8_t *payload, const uint64_t *off, const uint32_t *len,
+                  uint32_t n, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n == 0) return ZRC4_OK;
+    if (!ring || ring_cap == 0 || !rid || !pos || !payload || !off || !len) return ZRC4_ERR_INVALID_ARG;
+    int rc = set_device(c);
+    if (rc) return rc;
+    hipLaunchKernelGGL(zrc4::xor_ring_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, ring, ring_cap,
+                       rid, pos, payload, off, len, n);
+    return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
 }
 
 int zrc4_sync(zrc4_ctx *c, void *stream)

@@ -30,6 +30,14 @@ constexpr int kGroupBytes = 256 * 256; // 64 KiB S-box image per group
 
 enum : uint32_t { kErrSlotRange = 1u };
 
+// The fault latch lives in pinned host memory; every faulting lane stores the
+// same value, so a plain (non-atomic) system-visible store is enough and the
+// host reads it after its stream wait.
+__device__ __forceinline__ void latch_fault(uint32_t *err)
+{
+    __hip_atomic_store(err, kErrSlotRange, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t col_of(uint32_t j)
@@ -698,7 +706,7 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     const uint64_t myoff = valid ? off[e] : 0u;
     uint32_t slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
     if (valid && slot >= capacity) {
-        atomicOr(err, kErrSlotRange);
+        latch_fault(err);
         slot = ZRC4_INVALID;
     }
     const bool active = slot != ZRC4_INVALID;
@@ -804,7 +812,7 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     const bool valid = e < n;
     uint32_t slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
     if (valid && slot >= capacity) {
-        atomicOr(err, kErrSlotRange);
+        latch_fault(err);
         slot = ZRC4_INVALID;
     }
     const bool active = slot != ZRC4_INVALID;
@@ -860,6 +868,56 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         lds_to_image(arena + (size_t)g * kGroupBytes, S);
     } else if (active) {
         scatter_column(arena, slot, S, col);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// xor_ring_kernel: payload spans XOR pre-generated keystream from per-slot
+// device rings (the session engine's latency path, zrc4_xor_ring).
+// One workgroup per entry.  Payload is walked in dwords aligned to its own
+// address (whole dwords: one 4-byte RMW; the two edge dwords: byte RMWs, so no
+// byte outside the span is ever written); the ring is read bytewise at
+// (pos + i) mod cap and the bytes used are zeroed, so the next zrc4_crypt
+// over them (0 ^ k = k) refills pure keystream.  Consecutive lanes touch
+// consecutive dwords / ring bytes (coalesced).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+xor_ring_kernel(uint8_t *__restrict__ ring, uint32_t cap, const uint32_t *__restrict__ rid,
+                const uint32_t *__restrict__ pos, uint8_t *__restrict__ payload,
+                const uint64_t *__restrict__ off, const uint32_t *__restrict__ len, uint32_t n)
+{
+    const uint32_t e = blockIdx.x;
+    if (e >= n) return;
+    const uint32_t L = len[e];
+    if (L == 0) return;
+    uint8_t *d = payload + off[e];
+    uint8_t *r = ring + (size_t)rid[e] * cap;
+    const uint32_t p0 = pos[e];
+    const uint32_t head = (uint32_t)((uintptr_t)d & 3u);
+    uint8_t *d0 = d - head;
+    const uint32_t nwords = (head + L + 3u) >> 2;
+    for (uint32_t w = threadIdx.x; w < nwords; w += blockDim.x) {
+        uint32_t ks = 0, mask = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const int32_t idx = (int32_t)(w * 4u + j) - (int32_t)head;   // span byte index
+            if (idx >= 0 && (uint32_t)idx < L) {
+                uint32_t q = p0 + (uint32_t)idx;
+                if (q >= cap) q -= cap;
+                ks |= (uint32_t)r[q] << (8u * j);
+                r[q] = 0;
+                mask |= 0xFFu << (8u * j);
+            }
+        }
+        if (mask == 0xFFFFFFFFu) {
+            uint32_t *wp = reinterpret_cast<uint32_t *>(d0) + w;
+            *wp ^= ks;
+        } else {
+            uint8_t *bp = d0 + w * 4u;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (mask & (0xFFu << (8u * j))) bp[j] ^= (uint8_t)(ks >> (8u * j));
+        }
     }
 }
 
