@@ -439,6 +439,99 @@ def ksa_storm(args):
     return out
 
 
+# ------------------------------------------------- device-side framing scan
+def frame_payload(S: int, L: int, seed: int = 7):
+    """S session buffers of L bytes of proto4z packets (length fields drawn
+    from 6..min(700, L/2+6)), the last packet cut at the buffer end: what a
+    recv block holds after the decrypt.  Returns (buffers, complete packets)."""
+    rng = np.random.default_rng(seed)
+    buf = np.zeros(S * L, dtype=np.uint8)
+    hi = min(700, L // 2 + 6)
+    lens = rng.integers(6, hi + 1, size=(S, max(4, 2 * L // 6)))
+    complete = 0
+    for s in range(S):
+        pos, k = 0, 0
+        while pos + 4 <= L:
+            ln = int(lens[s, k % lens.shape[1]])
+            k += 1
+            buf[s * L + pos: s * L + pos + 4] = np.frombuffer(ln.to_bytes(4, "little"), np.uint8)
+            complete += pos + ln <= L
+            pos += ln
+    return buf, complete
+
+
+def frame_bench(args):
+    """SURVEY.md §8f row 4: zrc4_frame_scan (TcpSession::onRecv's framing loop,
+    src/frame/session.cpp:329-371, over HasRawPacket, proto4z.h:704-748) on
+    decrypted, device-resident buffers shaped like the workload; K launches
+    timed with HIP events over 16-launch segments, next to the crypt kernel on
+    the same batch.  CPU baseline: the oracle's scan, 1 thread (the reference
+    frames on its single event-loop thread).  Reported in DESIGN.md; never the
+    headline `value`."""
+    import torch
+    from zsummerx_amd import Context
+    S, L = CONFIG_SHAPES[args.workload]
+    S = min(S, 131072)
+    dev = torch.device("cuda", 0)
+    buf, npk_total = frame_payload(S, L)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_buf = T(buf)
+    d_off = T(np.arange(S, dtype=np.int64) * L)
+    d_len = T(np.full(S, L, dtype=np.int32))
+    npk, used, status = (torch.zeros(S, dtype=torch.int32, device=dev) for _ in range(3))
+    st = torch.cuda.current_stream(dev)
+    with Context(0, S) as ctx:
+        def timed(fn):
+            for _ in range(args.warmup):
+                fn()
+            torch.cuda.synchronize()
+            seg, done = [], 0
+            while done < args.steps:
+                m = min(args.event_every, args.steps - done)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(st)
+                for _ in range(m):
+                    fn()
+                b.record(st)
+                seg.append((a, b, m))
+                done += m
+            torch.cuda.synchronize()
+            return statistics.median(a.elapsed_time(b) / m for a, b, m in seg) * 1e-3
+        bound = max(20480, L)          # SESSION_BLOCK_SIZE (config.h:100); cfg4's 64 KiB needs a larger block
+        scan = lambda: ctx.frame_scan(d_buf, d_off, d_len, bound, npk, used, status, stream=st)
+        t_scan = timed(scan)
+        ctx.sync(st)
+        got_npk = int(npk.sum().item())
+        scratch = T(np.zeros(S * L, dtype=np.uint8))
+        t_crypt = timed(lambda: ctx.crypt_range(0, scratch, d_off, d_len, n=S, stream=st))
+        ctx.sync(st)
+    out = {"metric": "proto4z frame scan (device-resident, decrypted buffers)", "workload": args.workload,
+           "sessions": S, "bytes_per_session": L, "packets_per_launch": got_npk,
+           "packets_expected": npk_total, "kernel_us": round(t_scan * 1e6, 3),
+           "framed_gib_s": round(S * L / t_scan / GIB, 2), "packets_per_s": round(got_npk / t_scan, 1),
+           "crypt_kernel_us_same_batch": round(t_crypt * 1e6, 3),
+           "scan_share_of_decrypt_plus_scan": round(t_scan / (t_scan + t_crypt), 4),
+           "note": "scan reads 4 header bytes per packet; latency-bound chain of header reads per session"}
+    if args.cpu_seconds > 0:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import pyoracle  # cpu_baseline leg only
+        off = np.arange(S, dtype=np.uint64) * L
+        ln = np.full(S, L, dtype=np.uint32)
+        runs, t_end = [], time.perf_counter() + args.cpu_seconds
+        while len(runs) < 5 or time.perf_counter() < t_end:
+            t1 = time.perf_counter()
+            pyoracle.frame_scan(buf, off, ln, max(20480, L), 0)
+            runs.append(time.perf_counter() - t1)
+            if len(runs) >= 50:
+                break
+        cpu = statistics.median(runs)
+        out["cpu_baseline"] = {"value": round(S * L / cpu / GIB, 3), "unit": "GiB/s framed", "cores": 1,
+                               "kind": "port", "sample": f"the same {S} buffers, oracle_frame_scan, median of {len(runs)}"}
+        out["speedup_vs_1_core"] = round(cpu / t_scan, 1)
+    assert got_npk == npk_total, (got_npk, npk_total)
+    return out
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     p.add_argument("--gpus", type=int, default=1)
@@ -456,6 +549,8 @@ def parse(argv=None):
                    help="measure the PCIe-inclusive rate instead (DESIGN.md), one JSON line")
     p.add_argument("--ksa", action="store_true",
                    help="measure the connection-storm KSA rate instead (DESIGN.md), one JSON line")
+    p.add_argument("--frame", action="store_true",
+                   help="measure the device-side proto4z framing scan instead (DESIGN.md), one JSON line")
     p.add_argument("--chunks", type=int, default=8)
     p.add_argument("--streams", type=int, default=3)
     return p.parse_args(argv)
@@ -469,6 +564,9 @@ def main(argv=None):
         return
     if args.ksa:
         print(json.dumps(ksa_storm(args)), flush=True)
+        return
+    if args.frame:
+        print(json.dumps(frame_bench(args)), flush=True)
         return
     if ws != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE")

@@ -129,6 +129,23 @@ int zrc4_xor_ring(zrc4_ctx *ctx, uint8_t *ring, uint32_t ring_cap,
                   const uint64_t *off, const uint32_t *len, uint32_t n,
                   void *stream);
 
+/* Device-side proto4z framing of decrypted session buffers (the step after
+ * the recv decrypt, src/frame/session.cpp:329-371, with HasRawPacket,
+ * depends/proto4z/proto4z.h:704-748, as the check): entry i walks
+ * buf[off[i] .. off[i]+len[i]) from its start with the reference's
+ * check(begin+used, len-used, bound-used, bound) until it stops, and writes
+ *   npk[i]     complete packets found,
+ *   used[i]    bytes they cover (the reference memmoves the rest down),
+ *   status[i]  1 = stopped on shortage, 2 = on corruption (close the session),
+ *   pkt_len[i * max_packets + k]  the first max_packets packet lengths
+ *              (pkt_len may be NULL when max_packets == 0).
+ * bound is the receive block size (SESSION_BLOCK_SIZE = 20480 in the
+ * reference, config.h:100).  Device pointers; asynchronous on `stream`. */
+int zrc4_frame_scan(zrc4_ctx *ctx, const uint8_t *buf, const uint64_t *off,
+                    const uint32_t *len, uint32_t bound, uint32_t n,
+                    uint32_t max_packets, uint32_t *npk, uint32_t *used,
+                    uint32_t *status, uint32_t *pkt_len, void *stream);
+
 /* Wait for `stream`, then report (and clear) any latched device-side fault. */
 int zrc4_sync(zrc4_ctx *ctx, void *stream);
 

@@ -52,6 +52,7 @@ def lib():
         L.oracle_state_to_bytes.argtypes = [_P, _P, _P, _P]
         L.oracle_state_from_bytes.argtypes = [_P, _P, C.c_uint8, C.c_uint8]
         L.oracle_now.restype = C.c_double
+        L.oracle_frame_scan.argtypes = [_P, _P, _P, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P]
         _lib = L
     return _lib
 
@@ -67,6 +68,7 @@ def ref_lib():
         R.zrc4_ref_get_state.argtypes = [_P, _P, _P, _P]
         R.zrc4_ref_crypt_batch.argtypes = [_P, _P, _P, _P, C.c_uint32]
         R.zrc4_ref_crypt_batch.restype = C.c_double
+        R.zrc4_ref_has_raw_packet.argtypes = [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
         _ref = R
     return _ref
 
@@ -191,3 +193,59 @@ class Batch:
 
 def now() -> float:
     return lib().oracle_now()
+
+
+def frame_scan(buf: np.ndarray, off: np.ndarray, length: np.ndarray, bound: int, max_packets: int):
+    """oracle_frame_scan: (npk, used, status, pkt_len[n, max_packets])."""
+    n = int(length.size)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    npk, used, status = (np.zeros(n, dtype=np.uint32) for _ in range(3))
+    pk = np.zeros((n, max(1, max_packets)), dtype=np.uint32)
+    p = lambda a: C.c_void_p(a.ctypes.data)
+    lib().oracle_frame_scan(p(buf), p(off), p(length), int(bound), n, int(max_packets), p(npk), p(used),
+                            p(status), p(pk))
+    return npk, used, status, pk
+
+
+def py_frame_scan(data: bytes, bound: int):
+    """Pure-Python restatement for tiny cases (session.cpp:329-371 +
+    proto4z.h:704-748): list of packet lengths, used, status."""
+    used, out = 0, []
+    while True:
+        cur, bl = len(data) - used, bound - used
+        if bl < cur or bound < bl:
+            return out, used, 2
+        if cur < 6:
+            return out, used, 1
+        pl = int.from_bytes(data[used:used + 4], "little")
+        if pl < 6:
+            return out, used, 2
+        if pl > bl:
+            return out, used, (2 if pl > bound else 1)
+        if pl > bound:
+            return out, used, 2
+        if pl > cur:
+            return out, used, 1
+        out.append(pl)
+        used += pl
+
+
+def ref_frame_scan(data: bytes, bound: int):
+    """The onRecv framing loop (src/frame/session.cpp:329-371) driven by the
+    REAL reference HasRawPacket (oracle/_ref): (packet lengths, used, status)."""
+    R = ref_lib()
+    if R is None:
+        raise FileNotFoundError(f"{REF_LIB} not built (needs /root/reference)")
+    buf = _buf(data)
+    base = C.addressof(buf)
+    used, out = 0, []
+    while True:
+        second = C.c_uint32()
+        st = R.zrc4_ref_has_raw_packet(C.c_void_p(base + used), len(data) - used, bound - used, bound,
+                                       C.byref(second))
+        if st != 0:
+            return out, used, st
+        out.append(second.value)
+        used += second.value

@@ -131,3 +131,55 @@ double oracle_now(void)
     clock_gettime(CLOCK_MONOTONIC, &ts);
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
+
+/* proto4z HasRawPacket (depends/proto4z/proto4z.h:704-748), restated:
+ * 0 intact (*plen = packet length), 1 shortage, 2 corrupted.  The header
+ * length it checks against is sizeof(LenInteger) + sizeof(ProtoInteger) = 6,
+ * and the length field is a little-endian u32 (ReadPodData, :684-689). */
+static int has_raw_packet(const uint8_t *b, uint32_t cur, uint32_t boundLen, uint32_t maxLen, uint32_t *plen)
+{
+    if (boundLen < cur || maxLen < boundLen)
+        return 2;
+    if (cur < 6)
+        return 1;
+    uint32_t pl = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+    if (pl < 6)
+        return 2;
+    if (pl > boundLen)
+        return pl > maxLen ? 2 : 1;
+    if (pl > maxLen)
+        return 2;
+    if (pl <= cur) {
+        *plen = pl;
+        return 0;
+    }
+    return 1;
+}
+
+/* TcpSession::onRecv's framing loop (src/frame/session.cpp:329-371, PT_TCP):
+ * walk session i's buffer buf[off[i] .. off[i]+len[i]) with
+ * check(begin+used, len-used, bound-used, bound) until shortage (status 1) or
+ * corruption (status 2); npk = packets found, used = bytes they cover, the
+ * first max_packets lengths go to pkt_len[i*max_packets ..]. */
+void oracle_frame_scan(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint32_t bound,
+                       uint32_t n, uint32_t max_packets, uint32_t *npk, uint32_t *used,
+                       uint32_t *status, uint32_t *pkt_len)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t *b = buf + off[i];
+        uint32_t u = 0, k = 0, st;
+        for (;;) {
+            uint32_t pl = 0;
+            st = (uint32_t)has_raw_packet(b + u, len[i] - u, bound - u, bound, &pl);
+            if (st != 0)
+                break;
+            if (pkt_len && k < max_packets)
+                pkt_len[(size_t)i * max_packets + k] = pl;
+            ++k;
+            u += pl;
+        }
+        npk[i] = k;
+        used[i] = u;
+        status[i] = st;
+    }
+}

@@ -55,6 +55,14 @@ void oracle_state_to_bytes(const oracle_rc4_state *st, uint8_t sbox[256],
 void oracle_state_from_bytes(oracle_rc4_state *st, const uint8_t sbox[256],
                              uint8_t x, uint8_t y);
 
+/* proto4z framing of n decrypted session buffers, as TcpSession::onRecv does
+ * after decrypting (src/frame/session.cpp:329-371 with HasRawPacket,
+ * depends/proto4z/proto4z.h:704-748): status 1 = stopped on shortage, 2 = on
+ * corruption; npk / used / pkt_len as zrc4_frame_scan (include/zrc4.h). */
+void oracle_frame_scan(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint32_t bound,
+                       uint32_t n, uint32_t max_packets, uint32_t *npk, uint32_t *used,
+                       uint32_t *status, uint32_t *pkt_len);
+
 /* Wall-clock seconds (CLOCK_MONOTONIC) for the cpu_baseline timer. */
 double oracle_now(void);
 

@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <chrono>
 #include <rc4/rc4_encryption.h>
+#include <proto4z/proto4z.h>   // HasRawPacket (depends/proto4z/proto4z.h:704-748), header-only
 
 static_assert(sizeof(RC4Encryption) == 2 * sizeof(int) + 256 * sizeof(int),
               "reference state is int _x, _y, _box[256] (rc4_encryption.h:96-98)");
@@ -56,6 +57,18 @@ double zrc4_ref_crypt_batch(void *states, uint8_t *payload, const uint64_t *off,
     for (uint32_t i = 0; i < n; ++i) s[i].encryption(payload + off[i], (int)len[i]);
     auto t1 = std::chrono::steady_clock::now();
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// zsummer::proto4z::HasRawPacket -- the reference's framing check, as
+// TcpSession::onRecv calls it through DefaultRawPacketCheck
+// (include/zsummerX/frame/manager.h:53-57).  Returns the IntegrityType
+// (0 intact, 1 shortage, 2 corrupted) and its length result in *second.
+int zrc4_ref_has_raw_packet(const uint8_t *buff, uint32_t cur, uint32_t bound_len, uint32_t max_len,
+                            uint32_t *second)
+{
+    auto r = zsummer::proto4z::HasRawPacket(reinterpret_cast<const char *>(buff), cur, bound_len, max_len);
+    *second = r.second;
+    return (int)r.first;
 }
 
 }  // extern "C"

@@ -19,6 +19,8 @@ Outputs (all small):
                     pre-advance, ragged lengths and unaligned offsets
   synth_digests.json  SHA-256 of ciphertext + final states of the synthetic
                     bench workloads cfg2..cfg5 (full BASELINE sizes)
+  frame.json        proto4z framing cases: the reference HasRawPacket
+                    (proto4z.h:704-748) driven by the onRecv loop
 """
 from __future__ import annotations
 
@@ -208,12 +210,41 @@ def gen_synth_digests():
     return res
 
 
+def frame_cases():
+    """Decrypted session buffers for the framing scan (row 4): valid packet
+    streams ending in a partial packet or exactly, corrupt length fields
+    (< 6, > bound, > maxBuffLen), headers split at every position, empty."""
+    rng = random.Random(77)
+    hdr = lambda n, proto=1: n.to_bytes(4, "little") + (0).to_bytes(2, "little") + proto.to_bytes(2, "little")
+    pk = lambda n: hdr(n) + bytes(rng.getrandbits(8) for _ in range(n - 8))
+    cases = [("empty", b"", 20480), ("five_bytes", b"\x10\x00\x00\x00\x00", 20480),
+             ("one_exact", pk(100), 20480), ("min_header", hdr(6)[:6], 20480), ("len_5", hdr(5) + b"zz", 20480),
+             ("len_0", hdr(0), 20480), ("len_gt_bound", hdr(30000) + b"q" * 40, 20480),
+             ("len_gt_room", hdr(20000) + b"q" * 40, 20480), ("bound_lt_len_field", pk(64) + pk(64), 100),
+             ("two_then_partial", pk(300) + pk(9) + pk(1000)[:500], 20480),
+             ("exact_bound", pk(20480), 20480), ("corrupt_after_two", pk(50) + pk(60) + hdr(3) + b"abc", 20480)]
+    for k in range(20):
+        stream = b"".join(pk(rng.choice([6, 8, 9, 64, 700, 1500, rng.randint(6, 4000)])) for _ in range(rng.randint(0, 12)))
+        cut = rng.randint(0, len(stream)) if stream else 0
+        cases.append((f"random_{k}", stream[: max(cut, len(stream) - rng.randint(0, 30))], 20480))
+    out = []
+    for name, data, bound in cases:
+        data = data[:bound] if len(data) > bound else data
+        pkts, used, status = pyoracle.ref_frame_scan(data, bound)
+        out.append({"name": name, "data": data.hex(), "bound": bound, "packets": pkts, "used": used,
+                    "status": status})
+    return {"source": "zsummer::proto4z::HasRawPacket (depends/proto4z/proto4z.h:704-748) compiled from "
+                      "/root/reference via oracle/ref_shim.cpp, driven by the onRecv loop "
+                      "(src/frame/session.cpp:329-371)", "cases": out}
+
+
 def main():
     if pyoracle.ref_lib() is None:
         sys.exit("oracle/_ref/libzrc4_ref.so missing: run `make -C oracle` with /root/reference present")
     (OUT / "kat.json").write_text(json.dumps(gen_kat(), indent=1) + "\n")
     (OUT / "edge.json").write_text(json.dumps(gen_edge(), indent=1) + "\n")
     gen_batch_small()
+    (OUT / "frame.json").write_text(json.dumps(frame_cases(), indent=1) + "\n")
     if "--no-synth" not in sys.argv:
         (OUT / "synth_digests.json").write_text(json.dumps(gen_synth_digests(), indent=1) + "\n")
     print("golden fixtures written to", OUT)

@@ -1,0 +1,165 @@
+"""Device-side proto4z framing: zrc4_frame_scan walks
+decrypted session buffers exactly as TcpSession::onRecv's framing loop
+(src/frame/session.cpp:329-371) drives HasRawPacket
+(depends/proto4z/proto4z.h:704-748).
+
+Pinned by tests/golden/frame.json, generated from the REAL reference
+HasRawPacket compiled from /root/reference (oracle/ref_shim.cpp)."""
+import random
+import struct
+
+import numpy as np
+import pytest
+
+import pyoracle
+
+BOUND = 20480
+
+
+def pack_cases(frame_golden):
+    cases = frame_golden["cases"]
+    datas = [bytes.fromhex(c["data"]) for c in cases]
+    off = np.zeros(len(datas), dtype=np.uint64)
+    acc = 0
+    for i, d in enumerate(datas):
+        off[i] = acc
+        acc += len(d) + 3                       # odd spacing: headers land at every alignment
+    buf = np.zeros(acc + 8, dtype=np.uint8)
+    for i, d in enumerate(datas):
+        buf[int(off[i]):int(off[i]) + len(d)] = np.frombuffer(d, np.uint8)
+    return cases, buf, off, np.array([len(d) for d in datas], dtype=np.uint32)
+
+
+def packet_streams(n, avg_len, seed, max_pk=4000):
+    """n session buffers of proto4z packets, each ending in a partial packet
+    or exactly, plus a few corrupt ones."""
+    rng = random.Random(seed)
+    bufs = []
+    for i in range(n):
+        out = bytearray()
+        target = rng.randint(0, 2 * avg_len)
+        while len(out) < target:
+            ln = rng.choice([6, 8, 9, 33, 64, 200, 700, rng.randint(6, max_pk)])
+            out += struct.pack("<IHH", ln, 0, 7)[: min(8, ln)] + bytes(max(0, ln - 8))
+        cut = len(out) - rng.randint(0, 20) if out and rng.random() < 0.7 else len(out)
+        b = bytes(out[:max(cut, 0)])
+        if rng.random() < 0.05 and len(b) > 10:           # corrupt a length field
+            b = struct.pack("<I", rng.choice([0, 3, 5, 30000, 1 << 30])) + b[4:]
+        bufs.append(b[:BOUND])
+    off = np.zeros(n, dtype=np.uint64)
+    acc = 0
+    for i, b in enumerate(bufs):
+        off[i] = acc
+        acc += len(b) + (i % 5)
+    buf = np.zeros(acc + 8, dtype=np.uint8)
+    for i, b in enumerate(bufs):
+        buf[int(off[i]):int(off[i]) + len(b)] = np.frombuffer(b, np.uint8)
+    return buf, off, np.array([len(b) for b in bufs], dtype=np.uint32)
+
+
+@pytest.fixture(scope="module")
+def frame_golden():
+    import json
+    from conftest import GOLDEN
+    return json.loads((GOLDEN / "frame.json").read_text())
+
+
+# ------------------------------------------------------------------ CPU
+def test_oracle_scan_matches_reference_fixtures(frame_golden):
+    cases, buf, off, ln = pack_cases(frame_golden)
+    npk, used, status, pk = pyoracle.frame_scan(buf, off, ln, BOUND, 16)
+    for i, c in enumerate(cases):
+        if c["bound"] != BOUND:
+            continue
+        assert (int(npk[i]), int(used[i]), int(status[i])) == (len(c["packets"]), c["used"], c["status"]), c["name"]
+        assert list(pk[i][: min(16, len(c["packets"]))]) == c["packets"][:16], c["name"]
+
+
+def test_py_restatement_matches_reference_fixtures(frame_golden):
+    for c in frame_golden["cases"]:
+        assert pyoracle.py_frame_scan(bytes.fromhex(c["data"]), c["bound"]) == (c["packets"], c["used"], c["status"])
+
+
+def test_oracle_scan_matches_real_reference_random():
+    if pyoracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    buf, off, ln = packet_streams(300, 1500, seed=3)
+    npk, used, status, pk = pyoracle.frame_scan(buf, off, ln, BOUND, 64)
+    for i in range(300):
+        data = buf[int(off[i]):int(off[i]) + int(ln[i])].tobytes()
+        pkts, u, st = pyoracle.ref_frame_scan(data, BOUND)
+        assert (int(npk[i]), int(used[i]), int(status[i])) == (len(pkts), u, st)
+        assert list(pk[i][: min(64, len(pkts))]) == pkts[:64]
+
+
+# ------------------------------------------------------------------ GPU
+def device_scan(torch, c, buf, off, ln, bound, maxp):
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+    n = ln.size
+    npk, used, status = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    pk = torch.zeros(max(1, n * maxp), dtype=torch.int32, device="cuda")
+    c.frame_scan(T(buf), T(off.view(np.int64)), T(ln.view(np.int32)), bound, npk, used, status,
+                 pk if maxp else None, maxp)
+    c.sync()
+    return (npk.cpu().numpy().view(np.uint32), used.cpu().numpy().view(np.uint32),
+            status.cpu().numpy().view(np.uint32), pk.cpu().numpy().view(np.uint32)[: n * maxp].reshape(n, maxp))
+
+
+@pytest.mark.gpu
+def test_device_scan_matches_reference_fixtures(built, frame_golden):
+    import torch
+    from zsummerx_amd import Context
+    cases, buf, off, ln = pack_cases(frame_golden)
+    with Context(0, 256) as c:
+        for bound in sorted({cs["bound"] for cs in cases}):
+            idx = [i for i, cs in enumerate(cases) if cs["bound"] == bound]
+            npk, used, status, pk = device_scan(torch, c, buf, off[idx], ln[idx], bound, 16)
+            for j, i in enumerate(idx):
+                cs = cases[i]
+                assert (int(npk[j]), int(used[j]), int(status[j])) == (len(cs["packets"]), cs["used"], cs["status"]), cs["name"]
+                assert list(pk[j][: min(16, len(cs["packets"]))]) == cs["packets"][:16], cs["name"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,avg,maxp", [(4096, 1024, 8), (65536, 256, 4), (1024, 16384, 64)])
+def test_device_scan_matches_oracle_at_baseline_shapes(built, n, avg, maxp):
+    import torch
+    from zsummerx_amd import Context
+    buf, off, ln = packet_streams(n, avg, seed=n)
+    want = pyoracle.frame_scan(buf, off, ln, BOUND, maxp)
+    with Context(0, 256) as c:
+        got = device_scan(torch, c, buf, off, ln, BOUND, maxp)
+    for w, g, name in zip(want, got, ["npk", "used", "status", "pkt_len"]):
+        assert np.array_equal(w, g), name
+
+
+@pytest.mark.gpu
+def test_decrypt_then_scan_pipeline(built):
+    """Ciphertext (oracle RC4 over packet streams) -> zrc4_crypt on the GPU ->
+    zrc4_frame_scan on the GPU, against the oracle doing both on the CPU."""
+    import torch
+    from zsummerx_amd import Context
+    n = 2048
+    buf, off, ln = packet_streams(n, 900, seed=11)
+    rng = np.random.default_rng(2)
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(n)]
+    ct = buf.copy()
+    for i in range(n):
+        a, z = int(off[i]), int(off[i]) + int(ln[i])
+        ct[a:z] = np.frombuffer(pyoracle.Rc4(keys[i]).encryption(ct[a:z].tobytes()), np.uint8)
+    want = pyoracle.frame_scan(buf, off, ln, BOUND, 8)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+    with Context(0, n) as c:
+        c.ksa_host(keys)
+        d = T(ct)
+        d_off, d_len = T(off.view(np.int64)), T(ln.view(np.int32))
+        c.crypt(d, d_off, d_len)
+        npk, used, status = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+        pk = torch.zeros(n * 8, dtype=torch.int32, device="cuda")
+        c.frame_scan(d, d_off, d_len, BOUND, npk, used, status, pk, 8)
+        c.sync()
+        assert np.array_equal(d.cpu().numpy(), buf)
+        got = (npk.cpu().numpy().view(np.uint32), used.cpu().numpy().view(np.uint32),
+               status.cpu().numpy().view(np.uint32), pk.cpu().numpy().view(np.uint32).reshape(n, 8))
+    for w, g, name in zip(want, got, ["npk", "used", "status", "pkt_len"]):
+        assert np.array_equal(w, g), name

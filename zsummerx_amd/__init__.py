@@ -104,6 +104,14 @@ class Context:
         check(self._lib.zrc4_xor_ring(self._h, _ptr(ring), int(ring_cap), _ptr(rid), _ptr(pos), _ptr(payload),
                                       _ptr(off), _ptr(length), n, _stream(stream)), "zrc4_xor_ring")
 
+    def frame_scan(self, buf, off, length, bound: int, npk, used, status, pkt_len=None, max_packets: int = 0,
+                   n=None, stream=None) -> None:
+        """zrc4_frame_scan: proto4z framing of decrypted buffers (device pointers)."""
+        n = int(length.numel() if n is None else n)
+        check(self._lib.zrc4_frame_scan(self._h, _ptr(buf), _ptr(off), _ptr(length), int(bound), n,
+                                        int(max_packets), _ptr(npk), _ptr(used), _ptr(status), _ptr(pkt_len),
+                                        _stream(stream)), "zrc4_frame_scan")
+
     def sync(self, stream=None) -> None:
         check(self._lib.zrc4_sync(self._h, _stream(stream)), "zrc4_sync")
 

@@ -224,6 +224,21 @@ int zrc4_xor_ring(zrc4_ctx *c, uint8_t *ring, uint32_t ring_cap, const uint32_t 
     return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
 }
 
+int zrc4_frame_scan(zrc4_ctx *c, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
+                    uint32_t bound, uint32_t n, uint32_t max_packets, uint32_t *npk, uint32_t *used,
+                    uint32_t *status, uint32_t *pkt_len, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n == 0) return ZRC4_OK;
+    if (!buf || !off || !len || !npk || !used || !status || (max_packets && !pkt_len))
+        return ZRC4_ERR_INVALID_ARG;
+    int rc = set_device(c);
+    if (rc) return rc;
+    hipLaunchKernelGGL(zrc4::frame_scan_kernel, dim3((n + 255u) / 256u), dim3(256), 0, (hipStream_t)stream,
+                       buf, off, len, bound, n, max_packets, npk, used, status, max_packets ? pkt_len : nullptr);
+    return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
+}
+
 int zrc4_sync(zrc4_ctx *c, void *stream)
 {
     if (!c) return ZRC4_ERR_INVALID_ARG;

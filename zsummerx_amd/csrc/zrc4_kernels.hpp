@@ -921,6 +921,51 @@ xor_ring_kernel(uint8_t *__restrict__ ring, uint32_t cap, const uint32_t *__rest
     }
 }
 
+// ---------------------------------------------------------------------------
+// frame_scan_kernel: proto4z framing of decrypted session buffers, device
+// side.  TcpSession::onRecv's loop
+// (src/frame/session.cpp:329-371) over HasRawPacket
+// (depends/proto4z/proto4z.h:704-748): walk from the buffer start, one packet
+// per check, until shortage (status 1) or corruption (status 2).  One lane per
+// session: the walk is a chain of dependent header reads (4 byte loads each,
+// headers sit at any alignment), so lanes run independent sessions side by
+// side.  Bytes past the last header read are never touched.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t load_le32(const uint8_t *p)
+{
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__global__ void __launch_bounds__(256)
+frame_scan_kernel(const uint8_t *__restrict__ buf, const uint64_t *__restrict__ off,
+                  const uint32_t *__restrict__ len, uint32_t bound, uint32_t n, uint32_t maxp,
+                  uint32_t *__restrict__ npk, uint32_t *__restrict__ used, uint32_t *__restrict__ status,
+                  uint32_t *__restrict__ pkt_len)
+{
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const uint8_t *b = buf + off[e];
+    const uint32_t L = len[e];
+    const uint32_t headLen = 4u + 2u;          // sizeof(LenInteger) + sizeof(ProtoInteger), proto4z.h:714
+    uint32_t u = 0, k = 0, st;
+    for (;;) {
+        const uint32_t cur = L - u, bl = bound - u;
+        if (bl < cur || bound < bl) { st = 2u; break; }              // :708-711
+        if (cur < headLen) { st = 1u; break; }                       // :715-718
+        const uint32_t pl = load_le32(b + u);                        // ReadPodData, :717
+        if (pl < headLen) { st = 2u; break; }                        // :718-721
+        if (pl > bl) { st = pl > bound ? 2u : 1u; break; }          // :722-732
+        if (pl > bound) { st = 2u; break; }                          // :735-738
+        if (pl > cur) { st = 1u; break; }                            // :747
+        if (pkt_len && k < maxp) pkt_len[(size_t)e * maxp + k] = pl;
+        ++k;
+        u += pl;
+    }
+    npk[e] = k;
+    used[e] = u;
+    status[e] = st;
+}
+
 // identity_kernel: every slot of every group gets the identity S-box (row k of
 // a group image is 256 copies of k).  One workgroup per group.
 __global__ void __launch_bounds__(256)
