@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--footprint-mib", type=int, default=640)
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--ksa", action="store_true", help="also time zrc4_ksa_range per variant")
     ap.add_argument("--no-check", action="store_true", help="timing-only ablation builds (outputs differ)")
     args = ap.parse_args()
 
@@ -106,6 +107,23 @@ def main():
                 ref = buf
             elif not args.no_check and not torch.equal(ref, buf):
                 raise SystemExit(f"variant {name} output differs from {libs[0][0]} on {wl}")
+        if args.ksa:
+            # connection-storm KSA timing: the batch-0 sessions re-seeded per launch
+            kt = {name: [] for name, _ in libs}
+            for r in range(args.rounds):
+                for (name, lib), h in zip(libs, ctxs):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    for i in range(args.launches):
+                        _capi.check(lib.zrc4_ksa_range(h, 0, C.c_void_p(keys.data_ptr()), C.c_void_p(koff.data_ptr()),
+                                                       C.c_void_p(klen.data_ptr()), S, st), f"{name} ksa")
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    kt[name].append(e0.elapsed_time(e1) * 1e3 / args.launches)
+            report[wl + "_ksa"] = {name: {"median_us": round(statistics.median(t), 2), "min_us": round(min(t), 2),
+                                          "streams_per_s": round(S / (statistics.median(t) * 1e-6), 1)}
+                                   for name, t in kt.items()}
+            print(wl + "_ksa", json.dumps(report[wl + "_ksa"]), flush=True)
         times = {name: [] for name, _ in libs}
         step = 1
         for r in range(args.rounds):

@@ -797,7 +797,57 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 
 // ---------------------------------------------------------------------------
 // ksa_kernel: batched RC4Encryption::makeSBox (rc4_encryption.h:46-72).
+//
+// The swap step is the PRGA swap without the keystream read, plus a key
+// byte, so it uses the same 16-bit LDS addresses (index in byte 1) and SDWA
+// byte-1 adds.  Per step i (hand-written, ZRC4_KSA_STEP):
+//     j += a                      (j already holds j + key[k], added while the
+//                                  previous step waited for S[i])
+//     b = S[j] ; S[j] = a ; p = S[i+1] ; S[i] = b
+//     j += key[k+1]
+// 3 VALU + 4 LDS + 2 waits; S[i+1] is read after the S[j] = a write, so no
+// forwarding is needed (S[i] = b goes to i != i+1).  Writing S[j] before S[i]
+// swaps the reference's order (:63-64); they only collide when i == j, and
+// then b == a.  Key bytes for 16 steps are fetched one chunk ahead.
 // ---------------------------------------------------------------------------
+#define ZRC4_KSA_STEP(XC, XN, A, P, KN)                                                          \
+    "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
+    "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
+    "ds_read_u8 %[b], %[ya]\n\t"                                                                 \
+    "ds_write_b8 %[ya], %[" #A "]\n\t"                                                           \
+    "ds_read_u8 %[" #P "], %[" #XN "]\n\t"                                                       \
+    "v_add_u32_sdwa %[ya], %[ya], %[" #KN "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "         \
+    "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
+    "s_waitcnt lgkmcnt(2)\n\t"                                                                   \
+    "ds_write_b8 %[" #XC "], %[b]\n\t"                                                           \
+    "v_add_u32_sdwa %[" #XC "], 1, %[" #XN "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "        \
+    "src0_sel:DWORD src1_sel:BYTE_1\n\t"                                                         \
+    "s_waitcnt lgkmcnt(1)\n\t"
+#define ZRC4_KSA_PAIR(K1, K2)                                                                    \
+    ZRC4_KSA_STEP(x0, x1, a0, a1, K1) ZRC4_KSA_STEP(x1, x0, a1, a0, K2)
+
+// 16 KSA steps.  In: x0 = &S[i], x1 = &S[i+1], a0 = S[i], ya = &S[j + key[i]].
+// kn[u] = key byte of step i+u+1 (kn[15] = first byte of the next chunk).
+__device__ __forceinline__ void ksa16_asm(uint32_t &x0, uint32_t &x1, uint32_t &a0, uint32_t &ya,
+                                          const uint32_t (&kn)[16])
+{
+    uint32_t a1, b;
+    asm volatile(
+        ZRC4_KSA_PAIR(k0, k1) ZRC4_KSA_PAIR(k2, k3) ZRC4_KSA_PAIR(k4, k5) ZRC4_KSA_PAIR(k6, k7)
+        ZRC4_KSA_PAIR(k8, k9) ZRC4_KSA_PAIR(k10, k11) ZRC4_KSA_PAIR(k12, k13) ZRC4_KSA_PAIR(k14, k15)
+        "s_waitcnt lgkmcnt(0)\n\t"
+        : [ya] "+v"(ya), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0), [a1] "=&v"(a1), [b] "=&v"(b)
+        : [k0] "v"(kn[0]), [k1] "v"(kn[1]), [k2] "v"(kn[2]), [k3] "v"(kn[3]), [k4] "v"(kn[4]),
+          [k5] "v"(kn[5]), [k6] "v"(kn[6]), [k7] "v"(kn[7]), [k8] "v"(kn[8]), [k9] "v"(kn[9]),
+          [k10] "v"(kn[10]), [k11] "v"(kn[11]), [k12] "v"(kn[12]), [k13] "v"(kn[13]),
+          [k14] "v"(kn[14]), [k15] "v"(kn[15])
+        : "memory");
+}
+
+#ifndef ZRC4_KSA_ASM
+#define ZRC4_KSA_ASM 1      // 0: the portable C step (A/B builds)
+#endif
+
 __global__ void __launch_bounds__(256, 2)
 ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
            const uint32_t *__restrict__ ids, uint32_t first_slot,
@@ -816,6 +866,8 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         slot = ZRC4_INVALID;
     }
     const bool active = slot != ZRC4_INVALID;
+    const uint32_t kl = active ? key_len[e] : 0u;
+    const uint8_t *key = active ? keys + key_off[e] : keys;
 
     bool whole;
     uint32_t g;
@@ -832,16 +884,53 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     const bool partial = (blockIdx.x + 1u) * kGroup > n;
     const uint32_t col = col_of(j);
 
-    if (whole && partial) {
-        image_to_lds(S, arena + (size_t)g * kGroupBytes);
+    // Identity boxes (:50-53): a whole, fully re-seeded group fills its 64 KiB
+    // image cooperatively (row k = 256 copies of k, 16 x 16 B per lane);
+    // otherwise each seeded lane writes its own column.
+    if (whole && !partial) {
+        uint4 *img = reinterpret_cast<uint4 *>(S);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t q = i * 256 + threadIdx.x;
+            const uint32_t v = (q >> 4) * 0x01010101u;
+            img[q] = make_uint4(v, v, v, v);
+        }
         __syncthreads();
+    } else {
+        if (whole && partial) {
+            image_to_lds(S, arena + (size_t)g * kGroupBytes);
+            __syncthreads();
+        }
+        if (active)
+            for (int k = 0; k < 256; ++k) S[(k << 8) | col] = (uint8_t)k;
     }
-    if (active) {
-        // identity box (:50-53)
-        for (int k = 0; k < 256; ++k) S[(k << 8) | col] = (uint8_t)k;
-        const uint32_t kl = key_len[e];
-        if (kl) {
-            const uint8_t *key = keys + key_off[e];
+
+    if (active && kl) {
+        if (ZRC4_KSA_ASM) {
+            // key bytes of steps 16c .. 16c+16, fetched one chunk ahead
+            uint32_t kk = 0;
+            auto fetch = [&](uint32_t (&kb)[17]) {
+#pragma unroll
+                for (int u = 0; u < 17; ++u) {
+                    kb[u] = key[kk];
+                    if (u < 16 && ++kk >= kl) kk = 0;   // key[k], k cycles mod len (:67-70)
+                }
+            };
+            uint32_t cur[17], nxt[17];
+            fetch(cur);
+            uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col], ya = col;
+            // j = 0 + key[0] before step 0 (the S[0] term is added inside the step)
+            ya = (ya & 0xFFu) | (((cur[0]) << 8) & 0xFF00u);
+            for (int c = 0; c < 16; ++c) {
+                if (c < 15) fetch(nxt);
+                uint32_t kn[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) kn[u] = cur[u + 1];
+                ksa16_asm(x0, x1, a0, ya, kn);
+#pragma unroll
+                for (int u = 0; u < 17; ++u) cur[u] = nxt[u];
+            }
+        } else {
             uint32_t jj = 0, kk = 0;
             for (int i0 = 0; i0 < 256; i0 += 16) {
                 uint32_t kb[16];
@@ -861,8 +950,8 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                 }
             }
         }
-        xy[slot] = 0;                                // _x = _y = 0 (:48-49)
     }
+    if (active) xy[slot] = 0;                        // _x = _y = 0 (:48-49)
     if (whole) {
         __syncthreads();
         lds_to_image(arena + (size_t)g * kGroupBytes, S);
