@@ -211,6 +211,49 @@ def test_slot_out_of_range_is_reported(ctx, torch_cuda):
     ctx.sync(s)  # latch cleared
 
 
+# ------------------------------------- throughput (staged) store path, ragged
+@pytest.mark.parametrize("ids_kind", ["range", "scattered"])
+def test_staged_path_ragged(built, torch_cuda, ids_kind):
+    """More than one workgroup per CU selects the throughput store path (the
+    DPP line loop, crypt_message_dpp).  Ragged lengths 0..699 (head bytes,
+    lines cut mid-way, 16-byte chunks and tail bytes), unaligned offsets with
+    gaps that must stay untouched, two calls in a row (state write-back),
+    whole-group images ("range") and per-lane gathers ("scattered" ids)."""
+    torch = torch_cuda
+    n = 70000                                     # 274 workgroups > 256 CUs
+    rng = np.random.default_rng(11 if ids_kind == "range" else 12)
+    keys = rng.integers(0, 256, 16 * n, dtype=np.uint8)
+    koff = np.arange(n, dtype=np.uint64) * 16
+    klen = np.full(n, 16, dtype=np.uint32)
+    ob = pyoracle.Batch(n)
+    ob.make_sbox(keys, koff, klen)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    ids = None if ids_kind == "range" else rng.permutation(n + 4000)[:n].astype(np.uint32)
+    s = torch.cuda.current_stream()
+    with Context(0, n + 4000) as c:
+        c.ksa(T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys),
+              ids=None if ids is None else T(ids.view(np.int32)), stream=s)
+        for call in range(2):
+            L = rng.integers(0, 700, n).astype(np.uint32)
+            gaps = rng.integers(0, 40, n)
+            off = np.cumsum(np.concatenate([[gaps[0]], L[:-1] + gaps[1:]])).astype(np.uint64)
+            data = rng.integers(0, 256, int(off[-1] + L[-1]) + 64, dtype=np.uint8)
+            want = data.copy()
+            ob.crypt(want, off, L, threads=8)
+            pay = T(data)
+            c.crypt(pay, T(off.view(np.int64)), T(L.view(np.int32)),
+                    ids=None if ids is None else T(ids.view(np.int32)), stream=s)
+            c.sync(s)
+            got = pay.cpu().numpy()
+            bad = np.flatnonzero(got != want)
+            assert bad.size == 0, (call, bad[:8], int(bad.size))
+        for i in (0, 1, n // 2, n - 1):
+            slot = i if ids is None else int(ids[i])
+            sb, x, y = c.get_state(slot)
+            want_sb, wx, wy = ob.state(i)
+            assert (sb, x, y) == (bytes(want_sb), wx, wy), i
+
+
 # ------------------------------------------------ full BASELINE-size configs
 def _device_workload(ctx, w, torch):
     dev = "cuda"

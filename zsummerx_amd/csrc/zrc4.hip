@@ -17,6 +17,8 @@ struct zrc4_ctx {
     uint32_t capacity;      // multiple of 256
     uint8_t *arena;         // capacity/256 groups x 64 KiB S-box images
     uint16_t *xy;           // per slot: x | y << 8
+    uint8_t *sink;          // crypt_kernel's per-thread sink slots (loads/stores past a
+                            // session's last block in the DPP line loop)
     uint32_t *err;          // latched device-side fault bits, in pinned host memory:
                             // kernels latch with a plain store, the host reads it
                             // after the stream wait (no read-back copy)
@@ -76,11 +78,11 @@ int launch_crypt(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, uint8_t 
     if (staged)
         hipLaunchKernelGGL(zrc4::crypt_kernel<true>, dim3(grid), dim3(zrc4::kGroup), 0, s,
                            c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
-                           c->err);
+                           c->err, c->sink);
     else
         hipLaunchKernelGGL(zrc4::crypt_kernel<false>, dim3(grid), dim3(zrc4::kGroup), 0, s,
                            c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
-                           c->err);
+                           c->err, c->sink);
     return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
 }
 
@@ -135,6 +137,7 @@ int zrc4_create(zrc4_ctx **out, int device, uint32_t capacity)
     const size_t groups = c->capacity / zrc4::kGroup;
     bool ok = hipMalloc(&c->arena, groups * (size_t)zrc4::kGroupBytes) == hipSuccess &&
               hipMalloc(&c->xy, (size_t)c->capacity * sizeof(uint16_t)) == hipSuccess &&
+              hipMalloc(&c->sink, zrc4::kSinkBytes) == hipSuccess &&
               hipHostMalloc(&c->err, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
               hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     if (!ok) { zrc4_destroy(c); return ZRC4_ERR_OUT_OF_MEMORY; }
@@ -160,6 +163,7 @@ int zrc4_destroy(zrc4_ctx *c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->arena) (void)hipFree(c->arena);
     if (c->xy) (void)hipFree(c->xy);
+    if (c->sink) (void)hipFree(c->sink);
     if (c->err) (void)hipHostFree(c->err);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);

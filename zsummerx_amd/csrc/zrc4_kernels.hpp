@@ -538,10 +538,6 @@ __device__ __forceinline__ void crypt_message_staged(uint8_t *S, uint8_t *stage,
     for (uint32_t i = 0; i < rem; ++i) t[i] ^= (uint8_t)prga_step(S, st);
 }
 
-#ifndef ZRC4_LINE_STORE
-#define ZRC4_LINE_STORE 1
-#endif
-
 __device__ __forceinline__ void load4(uint4 *q, const uint4 *p)
 {
 #pragma unroll
@@ -626,31 +622,40 @@ __device__ __forceinline__ void crypt_message_lines(uint8_t *S, uint8_t *stage, 
         uint4 v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = rslot[q * 64];
+        if (!(ZRC4_ABLATE & 1)) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            // chunk m lies in block b + (m >= 4) of the pair
-            if (b + (smask[r][q] >> 2) < snb[r][q])
-                *reinterpret_cast<gu32x4 *>(sbase[r][q] + b * 64u) = u32x4{v[q].x, v[q].y, v[q].z, v[q].w};
+            for (int q = 0; q < 4; ++q) {
+                // chunk m lies in block b + (m >= 4) of the pair
+                if (b + (smask[r][q] >> 2) < snb[r][q])
+                    *reinterpret_cast<gu32x4 *>(sbase[r][q] + b * 64u) = u32x4{v[q].x, v[q].y, v[q].z, v[q].w};
+            }
+        } else {
+            asm volatile("" :: "v"(v[0].x), "v"(v[1].x), "v"(v[2].x), "v"(v[3].x));
         }
         asm volatile("" ::: "memory");
     };
 
     uint4 A1[4], B0[4], B1[4];
     auto load_pair = [&](uint4 *d0, uint4 *d1, uint32_t b) {
+        if (ZRC4_ABLATE & 2) return;
         const uint32_t b0 = b < last ? b : last, b1 = b + 1u < last ? b + 1u : last;
         load4(d0, p + 4u * b0);
         load4(d1, p + 4u * b1);
     };
-    if (nblk) {
+    if (nblk && !(ZRC4_ABLATE & 2)) {
         if (!pre) load4(A, p);
         load4(A1, p + 4u * (1u < last ? 1u : last));
     }
     auto pair = [&](uint32_t b, uint4 *x0, uint4 *x1) {
         if (b < nblk) xor64_asm_p(st, x0);
         if (b + 1u < nblk) xor64_asm_p(st, x1);
-        swap_halves(x0, x1);
-        stage_round(0, x0, b);
-        stage_round(1, x1, b);
+        if ((ZRC4_ABLATE & 4) == 0) {
+            swap_halves(x0, x1);
+            stage_round(0, x0, b);
+            stage_round(1, x1, b);
+        } else {
+            asm volatile("" :: "v"(x0[0].x), "v"(x1[0].x), "v"(x0[3].w), "v"(x1[3].w));
+        }
     };
     for (uint32_t b = 0; b < wmax; b += 4) {
         if (nblk) load_pair(B0, B1, b + 2u);
@@ -670,6 +675,125 @@ __device__ __forceinline__ void crypt_message_lines(uint8_t *S, uint8_t *stage, 
     uint8_t *t = reinterpret_cast<uint8_t *>(p);
     for (uint32_t i = 0; i < rem; ++i) t[i] ^= (uint8_t)prga_step(S, st);
 }
+
+// ---------------------------------------------------------------------------
+// Throughput-regime message loop with an in-register transpose (the default
+// store path when two workgroups share a CU).
+//
+// Why: whole 128-byte lines are the only fast store shape (8 lanes per line:
+// 5.65 TB/s vs 0.96 TB/s for per-lane 16-B pieces, tools/ubench/lds_ubench.hip),
+// but a lane owns its own session's bytes.  crypt_message_lines gets there by
+// staging through LDS, which costs ~11 % extra LDS cycles in a kernel that is
+// LDS-bound at 8 waves/CU (ablation: profiles/r01_ab_ablation_v7.log).  Here
+// the 8x8 transpose of 16-byte chunks inside each group of 8 consecutive lanes
+// runs on VALU with v_cndmask_b32_dpp butterflies (96 VALU per line per lane,
+// no LDS), and the whole block loop is one asm statement generated by
+// tools/gen_line_loop.py (zrc4_line_loop.inc) so every VMEM op is issued with
+// the full exec mask and the vmcnt waits are exact static counts:
+//   * loads: the line two iterations ahead (blocks b+4, b+5), clamped to the
+//     lane's sink slot past its session's end;
+//   * stores: chunk i of the line of session 8g+q from lane 8g+i, or the sink
+//     past that session's last block (ragged batches);
+//   * exec is narrowed only around the keystream of each 64-byte block.
+// The caller preloads lines 0 and 1 (P, Q) before the S-box image fill.
+// ---------------------------------------------------------------------------
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+#include "zrc4_line_loop.inc"
+
+constexpr uint32_t kSinkSlot = 256;                 // bytes of sink per thread (128-B line + offsets)
+constexpr uint32_t kSinkBytes = kGroup * kSinkSlot; // one 64 KiB sink per context, shared by all workgroups
+
+// line = blocks at b0 (16 B x 4) and b1 (16 B x 4)
+__device__ __forceinline__ void preload_line(u32x32 &v, const uint8_t *b0, const uint8_t *b1)
+{
+    const u32x4 *p0 = reinterpret_cast<const u32x4 *>(b0);
+    const u32x4 *p1 = reinterpret_cast<const u32x4 *>(b1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const u32x4 t0 = p0[i], t1 = p1[i];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            v[4 * i + d] = t0[d];
+            v[16 + 4 * i + d] = t1[d];
+        }
+    }
+}
+
+__device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, u32x16 &addr,
+                                                const u32x8 &lim, uint64_t pa, uint32_t nblk,
+                                                uint32_t wmax, u32x2 sink)
+{
+    u32x16 X;
+    u32x8 T;
+    uint32_t b, k0, k1, a1s, sb, s1;
+    uint32_t palo = (uint32_t)pa, pahi = (uint32_t)(pa >> 32);
+    uint64_t full, msk;
+    asm volatile(
+        "s_mov_b64 %[full], exec\n\t"
+        "s_mov_b32 %[sb], 0\n\t"
+        "LL_LOOP_%=:\n\t"
+        ZRC4_LL_HALF_P
+        ZRC4_LL_HALF_Q
+        "s_branch LL_LOOP_%=\n\t"
+        "LL_DONE_%=:\n\t"
+        "s_mov_b64 exec, %[full]\n\t"
+        "s_nop 1\n\t"                          // store-data VGPRs: VMEM store -> VALU write hazard
+        : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1), [a0] "+v"(st.a0),
+          [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
+          [palo] "+v"(palo), [pahi] "+v"(pahi), [sb] "=&s"(sb), [s1] "=&s"(s1),
+          [full] "=&s"(full), [msk] "=&s"(msk),
+          "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
+          "=&{v[144:151]}"(T)
+        : [nblk] "v"(nblk), [wmax] "s"(wmax), "{v[136:143]}"(lim), "{v[152:153]}"(sink)
+        : "memory", "vcc", "scc");
+}
+
+__device__ __forceinline__ void crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8_t *msg, uint32_t len,
+                                                  u32x32 &P, u32x32 &Q, uint8_t *sinkp)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t head = head_bytes(msg, len);
+    for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
+    msg += head;
+    len -= head;
+    const uint32_t nblk = len >> 6;
+    const uint32_t wmax = __builtin_amdgcn_readfirstlane(wave_max(nblk));
+    if (wmax) {
+        // store role: lane 8g+i writes chunk i (16 B) of the line of session 8g+q
+        const uint32_t i = lane & 7u;
+        u32x16 addr;
+        u32x8 lim;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int src = (int)(lane & ~7u) | q;
+            const uint64_t a = __shfl((uint64_t)(uintptr_t)msg, src, 64) + 16u * i;
+            const uint32_t nb = __shfl(nblk, src, 64);
+            addr[2 * q] = (uint32_t)a;
+            addr[2 * q + 1] = (uint32_t)(a >> 32);
+            lim[q] = nb > (i >> 2) ? nb - (i >> 2) : 0u;      // store iff b + (i >= 4) < nb
+        }
+        const uint64_t s = (uint64_t)(uintptr_t)sinkp;
+        const u32x2 sink = {(uint32_t)s, (uint32_t)(s >> 32)};
+        crypt_lines_asm(st, P, Q, addr, lim, (uint64_t)(uintptr_t)msg + 256u, nblk, wmax, sink);
+    }
+    uint4 *p = reinterpret_cast<uint4 *>(msg + 64u * nblk);
+    uint32_t rem = len & 63u;
+    while (rem >= 16u) {
+        *p = xor16(S, st, *p);
+        ++p;
+        rem -= 16u;
+    }
+    uint8_t *t = reinterpret_cast<uint8_t *>(p);
+    for (uint32_t k = 0; k < rem; ++k) t[k] ^= (uint8_t)prga_step(S, st);
+}
+
+#ifndef ZRC4_STORE_PATH
+#define ZRC4_STORE_PATH 2    // staged launches: 0 quad stores via LDS, 1 line stores via LDS, 2 DPP transpose
+#endif
 
 // Which slot batch entry e maps to, and whether workgroup w owns one whole
 // aligned 256-slot group g (then state moves as a coalesced 64 KiB image).
@@ -692,11 +816,13 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
              const uint32_t *__restrict__ ids, uint32_t first_slot,
              uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
              const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
-             uint32_t *__restrict__ err)
+             uint32_t *__restrict__ err, uint8_t *__restrict__ sink)
 {
-    // one LDS object: 64 KiB S-box image + 4 x 4 KiB store staging (80 KiB,
-    // so two workgroups fill the CU's 160 KiB).  No other __shared__ object.
-    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kSmemBytes : kGroupBytes + 16];
+    // one LDS object: 64 KiB S-box image (+ 4 x 4 KiB store staging for the
+    // LDS-staged store paths: 80 KiB, so two workgroups fill the CU's 160 KiB).
+    constexpr bool kLdsStage = STAGED && ZRC4_STORE_PATH != 2;
+    constexpr bool kDpp = STAGED && ZRC4_STORE_PATH == 2;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsStage ? kSmemBytes : kGroupBytes + 16];
     uint8_t *S = smem;
 
     const uint32_t j = threadIdx.x;
@@ -734,7 +860,18 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     const uint32_t col = col_of(j);
     uint8_t *msg = payload + myoff;
     uint4 A[4];
-    const bool pre = active && mylen >= 64u && head_bytes(msg, mylen) == 0u;
+    const bool pre = !kDpp && active && mylen >= 64u && head_bytes(msg, mylen) == 0u;
+    u32x32 P, Q;
+    if constexpr (kDpp) {
+        // lines 0 and 1 of the message loop, issued ahead of the image fill
+        // (blocks past the session's end read the lane's sink slot)
+        const uint32_t h = head_bytes(msg, mylen);
+        const uint8_t *p = msg + h;
+        const uint32_t nb = (mylen - h) >> 6;
+        const uint8_t *sk = sink + (size_t)j * kSinkSlot;
+        preload_line(P, nb > 0 ? p : sk, nb > 1 ? p + 64 : sk + 64);
+        preload_line(Q, nb > 2 ? p + 128 : sk, nb > 3 ? p + 192 : sk + 64);
+    }
     if (whole) {
         if (!(ZRC4_ABLATE & 8)) {
         uint4 img[16];
@@ -767,7 +904,9 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         st.ya = (y << 8) | col;
         st.ta = col;
         st.x1 = col;
-        if (ZRC4_LINE_STORE)
+        if constexpr (kDpp)
+            crypt_message_dpp(S, st, msg, mylen, P, Q, sink + (size_t)j * kSinkSlot);
+        else if constexpr (ZRC4_STORE_PATH == 1)
             crypt_message_lines(S, smem + kGroupBytes + (j >> 6) * kStageBytes, st, msg, mylen, A, pre);
         else
             crypt_message_staged(S, smem + kGroupBytes + (j >> 6) * kStageBytes, st, msg, mylen, A, pre);
