@@ -254,7 +254,7 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic,
-                     "kernel": "zrc4::crypt_kernel",
+                     "kernel": kernel_name(S),
                      "algorithmic_bytes_per_launch": B,
                      "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                      "kernel_min_segment_us": round(min(kern_ms) * 1e3, 3),
@@ -264,6 +264,19 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
                                  "L70": round(latency_ceiling(S, L, 70), 1),
                                  "L130": round(latency_ceiling(S, L, 130), 1)},
     }
+
+
+def kernel_name(S: int) -> str:
+    """The kernel zrc4_crypt_range launches for S sessions (zrc4.hip
+    launch_crypt): more 256-session groups than CUs -> the persistent
+    throughput kernel, otherwise one group per workgroup."""
+    try:
+        import torch
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+    except Exception:
+        cus = 256
+    groups = -(-S // 256)
+    return "zrc4::crypt_stream_kernel<true>" if groups > cus else "zrc4::crypt_kernel<false>"
 
 
 def load_traffic(workload: str):

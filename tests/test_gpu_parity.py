@@ -214,13 +214,15 @@ def test_slot_out_of_range_is_reported(ctx, torch_cuda):
 # ------------------------------------- throughput (staged) store path, ragged
 @pytest.mark.parametrize("ids_kind", ["range", "scattered"])
 def test_staged_path_ragged(built, torch_cuda, ids_kind):
-    """More than one workgroup per CU selects the throughput store path (the
-    DPP line loop, crypt_message_dpp).  Ragged lengths 0..699 (head bytes,
-    lines cut mid-way, 16-byte chunks and tail bytes), unaligned offsets with
-    gaps that must stay untouched, two calls in a row (state write-back),
-    whole-group images ("range") and per-lane gathers ("scattered" ids)."""
+    """More than one workgroup per CU selects the throughput path
+    (crypt_stream_kernel: persistent over groups, DPP line loop).  Ragged
+    lengths 0..699 (head bytes, lines cut mid-way, 16-byte chunks and tail
+    bytes), unaligned offsets with gaps that must stay untouched, two calls
+    in a row (state write-back), whole-group images with prefetch ("range")
+    and per-lane gathers ("scattered" ids).  300 000 sessions = 1 172 groups,
+    so every workgroup of the 2-per-CU grid walks 2-3 groups."""
     torch = torch_cuda
-    n = 70000                                     # 274 workgroups > 256 CUs
+    n = 300000
     rng = np.random.default_rng(11 if ids_kind == "range" else 12)
     keys = rng.integers(0, 256, 16 * n, dtype=np.uint8)
     koff = np.arange(n, dtype=np.uint64) * 16

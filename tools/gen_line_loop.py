@@ -44,10 +44,12 @@ CTRL_B = {1: "quad_perm:[1,0,3,2]", 2: "quad_perm:[2,3,0,1]", 4: "row_shl:4"}   
 DPP_TAIL = "row_mask:0xf bank_mask:0xf bound_ctrl:1"
 
 
-def transpose_plan(cur_base: int):
-    """Emit the 3 butterfly stages; return (lines, final tuple base per chunk)."""
-    reg = {c: cur_base + 4 * c for c in range(8)}
-    free = [X_BASE + 4 * t for t in range(4)]
+def transpose_plan(start, free):
+    """Emit the 3 butterfly stages over chunk tuples start[c] (c = 0..7) with
+    the spare tuples `free`; return (lines, final chunk -> tuple map, ops,
+    tuples left free)."""
+    reg = dict(start)
+    free = list(free)
     lines, ops = [], []
     for m in (1, 2, 4):
         pairs = [(c, c | m) for c in range(8) if not c & m]
@@ -69,17 +71,17 @@ def transpose_plan(cur_base: int):
             free.append(reg[ca])
             reg[ca] = new[ca]
         lines.append("s_nop 1")
-    return lines, reg, ops
+    return lines, reg, ops, free
 
 
-def simulate(ops, cur_base: int, final):
+def simulate(ops, start, final):
     """Lane-level model of the emitted ops (tuple granularity, one value per
     (lane, chunk)): checks that lane 8g+i ends with chunk i of lane 8g+c in
     chunk slot c."""
     regs = {}
     for lane in range(64):
         for c in range(8):
-            regs[(cur_base + 4 * c, lane)] = (lane, c)
+            regs[(start[c], lane)] = (lane, c)
 
     def src(ctrl, lane):
         if ctrl.startswith("quad_perm"):
@@ -114,8 +116,9 @@ def zl_block(base: int) -> str:
 
 
 def half(name: str, cur: int) -> str:
-    tl, final, ops = transpose_plan(cur)
-    simulate(ops, cur, final)
+    start = {c: cur + 4 * c for c in range(8)}
+    tl, final, ops, _ = transpose_plan(start, [X_BASE + 4 * t for t in range(4)])
+    simulate(ops, start, final)
     q = lambda s: f'"{s}\\n\\t"'
     out = []
     w = out.append
@@ -183,10 +186,78 @@ def half(name: str, cur: int) -> str:
     return f"#define ZRC4_LL_HALF_{name} \\\n    " + " \\\n    ".join(out) + "\n"
 
 
+def half_coalesced(name: str, cur: int) -> str:
+    """Whole-line loads too: the line arrives as 8 loads of 8 lines each
+    (lane 8g+i: chunk i of session 8g+q's line in tuple q), a first transpose
+    gives every lane its own line, the keystream runs, a second transpose
+    turns it back for whole-line stores."""
+    start = {c: cur + 4 * c for c in range(8)}
+    ltl, lmap, lops, free = transpose_plan(start, [X_BASE + 4 * t for t in range(4)])
+    simulate(lops, start, lmap)
+    stl, smap, sops, _ = transpose_plan(lmap, free)
+    simulate(sops, lmap, smap)
+    q = lambda s: f'"{s}\\n\\t"'
+    out = []
+    w = out.append
+    # 1. this line's 8 loads: younger are the previous half's 8 stores and 8
+    #    loads -> vmcnt(16); the last half follows a half without loads: vmcnt(8)
+    w(q("s_add_u32 %[s1], %[sb], 2"))
+    w(q("s_cmp_ge_u32 %[s1], %[wmax]"))
+    w(q(f"s_cbranch_scc0 LC_{name}W_%="))
+    w(q("s_waitcnt vmcnt(8)"))
+    w(q(f"LC_{name}W_%=:"))
+    w(q("s_waitcnt vmcnt(16)"))
+    w(q("s_nop 1"))
+    for line in ltl:                                   # 2. lanes get their own line
+        w(q(line))
+    blk = lambda cs: "ZL_BLOCK(" + ", ".join(f"v{lmap[c] + d}" for c in cs for d in range(4)) + ")"
+    w(q("v_cmp_lt_u32_e64 %[msk], %[sb], %[nblk]"))     # 3. keystream, block b
+    w(q("s_and_b64 exec, %[full], %[msk]"))
+    w(q(f"s_cbranch_execz LC_{name}1_%="))
+    w(blk(range(4)))
+    w(q(f"LC_{name}1_%=:"))
+    w(q("s_add_u32 %[s1], %[sb], 1"))                  #    block b+1
+    w(q("v_cmp_lt_u32_e64 %[msk], %[s1], %[nblk]"))
+    w(q("s_and_b64 exec, %[full], %[msk]"))
+    w(q(f"s_cbranch_execz LC_{name}2_%="))
+    w(blk(range(4, 8)))
+    w(q(f"LC_{name}2_%=:"))
+    w(q("s_mov_b64 exec, %[full]"))
+    w(q("s_nop 4"))                                    # exec write -> DPP
+    for line in stl:                                   # 4. back to line-per-8-lanes
+        w(q(line))
+    for qq in range(8):                                # 5. whole-line stores
+        sa = SA0 if qq % 2 == 0 else SA1
+        a = ADDR_BASE + 2 * qq
+        w(q(f"v_cmp_gt_u32_e64 %[msk], v{LIM_BASE + qq}, %[sb]"))
+        w(q(f"v_cndmask_b32_e64 v{sa}, v{SINK}, v{a}, %[msk]"))
+        w(q(f"v_cndmask_b32_e64 v{sa + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
+        w(q(f"global_store_dwordx4 v[{sa}:{sa + 1}], v[{smap[qq]}:{smap[qq] + 3}], off"))
+    for qq in range(8):
+        a = ADDR_BASE + 2 * qq
+        w(q(f"v_lshl_add_u64 v[{a}:{a + 1}], 8, 4, v[{a}:{a + 1}]"))     # += 8 << 4 (shift must be 0..4)
+    # 6. whole-line loads of line b+4 (addresses now at line b+2: offset 128)
+    w(q("s_add_u32 %[s1], %[sb], 4"))
+    w(q("s_cmp_ge_u32 %[s1], %[wmax]"))
+    w(q(f"s_cbranch_scc1 LC_{name}L_%="))
+    for qq in range(8):
+        la = LA if qq % 2 == 0 else LB
+        a = ADDR_BASE + 2 * qq
+        w(q(f"v_cmp_gt_u32_e64 %[msk], v{LIM_BASE + qq}, %[s1]"))
+        w(q(f"v_cndmask_b32_e64 v{la}, v{SINK}, v{a}, %[msk]"))
+        w(q(f"v_cndmask_b32_e64 v{la + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
+        w(q(f"global_load_dwordx4 v[{cur + 4 * qq}:{cur + 4 * qq + 3}], v[{la}:{la + 1}], off offset:128"))
+    w(q(f"LC_{name}L_%=:"))
+    w(q("s_add_u32 %[sb], %[sb], 2"))
+    w(q("s_cmp_ge_u32 %[sb], %[wmax]"))
+    w(q("s_cbranch_scc1 LL_DONE_%="))
+    return f"#define ZRC4_LC_HALF_{name} \\\n    " + " \\\n    ".join(out) + "\n"
+
+
 def transpose_only(name: str, cur: int) -> str:
     """The butterflies alone + the final chunk -> tuple map, for
     tools/ubench/dpp_transpose_check.hip."""
-    tl, final, _ = transpose_plan(cur)
+    tl, final, _, _ = transpose_plan({c: cur + 4 * c for c in range(8)}, [X_BASE + 4 * t for t in range(4)])
     body = " \\\n    ".join(f'"{line}\\n\\t"' for line in tl)
     fin = ", ".join(str(final[c]) for c in range(8))
     return (f"#define ZRC4_LL_TRANSPOSE_{name} \\\n    {body}\n"
@@ -205,6 +276,8 @@ def main():
         "#pragma once\n",
         half("P", P_BASE),
         half("Q", Q_BASE),
+        half_coalesced("P", P_BASE),
+        half_coalesced("Q", Q_BASE),
         transpose_only("P", P_BASE),
     ]
     OUT.write_text("".join(text))

@@ -36,12 +36,14 @@ def main(src="gpurun_out/traffic", tag="r01"):
     calib_bytes = 1 << 30
     fetch_factor = statistics.median(v * 1024 / calib_bytes for _, v in calib)
     for wl in sys.argv[1:] or ["cfg2", "cfg5"]:
-        f = [v for n, v in per_dispatch(src / f"{wl}_FETCH_SIZE" / "run_counter_collection.csv", "crypt_kernel")][1:]
-        w = [v for n, v in per_dispatch(src / f"{wl}_WRITE_SIZE" / "run_counter_collection.csv", "crypt_kernel")][1:]
+        fr = per_dispatch(src / f"{wl}_FETCH_SIZE" / "run_counter_collection.csv", "zrc4::crypt_")[1:]
+        wr = per_dispatch(src / f"{wl}_WRITE_SIZE" / "run_counter_collection.csv", "zrc4::crypt_")[1:]
+        f, w = [v for _, v in fr], [v for _, v in wr]
+        kname = collections.Counter(n.split("(")[0].replace("void ", "") for n, _ in fr).most_common(1)[0][0]
         S, L = SHAPES[wl]
         fb, wb = statistics.median(f) * 1024, statistics.median(w) * 1024
         out = {
-            "kernel": "zrc4::crypt_kernel", "workload": wl, "dispatches": len(f),
+            "kernel": kname, "workload": wl, "dispatches": len(f),
             "fetch_size_bytes_raw": fb, "write_size_bytes_raw": wb,
             "fetch_factor_per_lane_16B_loads": round(fetch_factor, 4),
             "read_bytes": round(fb / fetch_factor), "write_bytes": round(wb),

@@ -9,7 +9,12 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <new>
+
+#ifndef ZRC4_PERSIST
+#define ZRC4_PERSIST 1
+#endif
 
 struct zrc4_ctx {
     int device;
@@ -75,11 +80,27 @@ int launch_crypt(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, uint8_t 
 #else
     const bool staged = grid > (uint32_t)c->num_cus;   // >1 workgroup per CU
 #endif
+#if ZRC4_STORE_PATH == 2
+    if (staged) {
+        // persistent over groups: 2 workgroups per CU (LDS- and VGPR-limited),
+        // each walking groups w, w + grid, ... (ZRC4_PERSIST=0: one group each)
+        const uint32_t wgs = ZRC4_PERSIST ? std::min(grid, 2u * (uint32_t)c->num_cus) : grid;
+        if (!ids && (first_slot & 255u) == 0u)
+            hipLaunchKernelGGL(zrc4::crypt_stream_kernel<true>, dim3(wgs), dim3(zrc4::kGroup), 0, s,
+                               c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
+                               c->err, c->sink);
+        else
+            hipLaunchKernelGGL(zrc4::crypt_stream_kernel<false>, dim3(wgs), dim3(zrc4::kGroup), 0, s,
+                               c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
+                               c->err, c->sink);
+    } else
+#else
     if (staged)
         hipLaunchKernelGGL(zrc4::crypt_kernel<true>, dim3(grid), dim3(zrc4::kGroup), 0, s,
                            c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
                            c->err, c->sink);
     else
+#endif
         hipLaunchKernelGGL(zrc4::crypt_kernel<false>, dim3(grid), dim3(zrc4::kGroup), 0, s,
                            c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
                            c->err, c->sink);

@@ -723,21 +723,92 @@ __device__ __forceinline__ void preload_line(u32x32 &v, const uint8_t *b0, const
     }
 }
 
-__device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, u32x16 &addr,
-                                                const u32x8 &lim, uint64_t pa, uint32_t nblk,
-                                                uint32_t wmax, u32x2 sink)
+// Loads stay per lane by default: whole-line loads (8 lanes per line, then a
+// second DPP transpose) measured 4 % slower on cfg5 (312.8 vs 300.2 us,
+// profiles/r01_ab_line_loads.log) -- per-lane 16-B loads already stream at
+// 5.5 TB/s and the extra 96 VALU per line cost more than they save.
+#ifndef ZRC4_LINE_LOADS
+#define ZRC4_LINE_LOADS 0    // 1: whole-line loads + a second transpose; 0: per-lane 16-B loads
+#endif
+
+// Everything about a group's messages the line loop needs that does not
+// depend on the S-boxes, so it can be computed (and the first two lines
+// loaded) before the group's S-box image is in LDS.
+//   p      the message after its unaligned head bytes, nblk its 64-byte blocks
+//   addr/lim  store (and, with line loads, load) role: lane 8g+i moves chunk
+//          i of the line of session 8g+q; lim_q = blocks of that session
+//          minus (i >= 4), so chunk i of the line at block b exists iff b < lim_q
+struct LineSetup {
+    u32x16 addr;
+    u32x8 lim;
+    uint64_t p;
+    uint32_t nblk, wmax;
+};
+
+__device__ __forceinline__ void line_setup(LineSetup &ls, const uint8_t *msg, uint32_t len)
+{
+    const uint32_t lane = threadIdx.x & 63u, i = lane & 7u;
+    const uint32_t h = head_bytes(msg, len);
+    ls.p = (uint64_t)(uintptr_t)(msg + h);
+    ls.nblk = (len - h) >> 6;
+    ls.wmax = __builtin_amdgcn_readfirstlane(wave_max(ls.nblk));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int src = (int)(lane & ~7u) | q;
+        const uint64_t a = __shfl(ls.p, src, 64) + 16u * i;
+        const uint32_t nb = __shfl(ls.nblk, src, 64);
+        ls.addr[2 * q] = (uint32_t)a;
+        ls.addr[2 * q + 1] = (uint32_t)(a >> 32);
+        ls.lim[q] = nb > (i >> 2) ? nb - (i >> 2) : 0u;
+    }
+}
+
+// Lines 0 and 1 in the layout the loop expects (sink past a session's end).
+__device__ __forceinline__ void preload_lines(u32x32 &P, u32x32 &Q, const LineSetup &ls, const uint8_t *sk)
+{
+#if ZRC4_LINE_LOADS
+    // tuple q = chunk i of the line of session 8g+q
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint8_t *a = reinterpret_cast<const uint8_t *>(
+            (uintptr_t)(((uint64_t)ls.addr[2 * q + 1] << 32) | ls.addr[2 * q]));
+        const u32x4 t0 = *reinterpret_cast<const u32x4 *>(ls.lim[q] > 0u ? a : sk);
+        const u32x4 t1 = *reinterpret_cast<const u32x4 *>(ls.lim[q] > 2u ? a + 128 : sk);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            P[4 * q + d] = t0[d];
+            Q[4 * q + d] = t1[d];
+        }
+    }
+#else
+    // the lane's own blocks 0..3
+    const uint8_t *p = reinterpret_cast<const uint8_t *>((uintptr_t)ls.p);
+    const uint32_t nb = ls.nblk;
+    preload_line(P, nb > 0 ? p : sk, nb > 1 ? p + 64 : sk + 64);
+    preload_line(Q, nb > 2 ? p + 128 : sk, nb > 3 ? p + 192 : sk + 64);
+#endif
+}
+
+__device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls, u32x2 sink)
 {
     u32x16 X;
     u32x8 T;
+    u32x16 addr = ls.addr;
     uint32_t b, k0, k1, a1s, sb, s1;
+    const uint64_t pa = ls.p + 256u;                 // per-lane loads: blocks 4, 5 next
     uint32_t palo = (uint32_t)pa, pahi = (uint32_t)(pa >> 32);
     uint64_t full, msk;
     asm volatile(
         "s_mov_b64 %[full], exec\n\t"
         "s_mov_b32 %[sb], 0\n\t"
         "LL_LOOP_%=:\n\t"
+#if ZRC4_LINE_LOADS
+        ZRC4_LC_HALF_P
+        ZRC4_LC_HALF_Q
+#else
         ZRC4_LL_HALF_P
         ZRC4_LL_HALF_Q
+#endif
         "s_branch LL_LOOP_%=\n\t"
         "LL_DONE_%=:\n\t"
         "s_mov_b64 exec, %[full]\n\t"
@@ -748,39 +819,24 @@ __device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &
           [full] "=&s"(full), [msk] "=&s"(msk),
           "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
           "=&{v[144:151]}"(T)
-        : [nblk] "v"(nblk), [wmax] "s"(wmax), "{v[136:143]}"(lim), "{v[152:153]}"(sink)
+        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), "{v[136:143]}"(ls.lim), "{v[152:153]}"(sink)
         : "memory", "vcc", "scc");
 }
 
+// One group's messages: head bytes, the line loop (lines 0 and 1 already in
+// P/Q), then 16-byte chunks and tail bytes.
 __device__ __forceinline__ void crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8_t *msg, uint32_t len,
-                                                  u32x32 &P, u32x32 &Q, uint8_t *sinkp)
+                                                  u32x32 &P, u32x32 &Q, const LineSetup &ls, uint8_t *sinkp)
 {
-    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t head = head_bytes(msg, len);
     for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
     msg += head;
     len -= head;
-    const uint32_t nblk = len >> 6;
-    const uint32_t wmax = __builtin_amdgcn_readfirstlane(wave_max(nblk));
-    if (wmax) {
-        // store role: lane 8g+i writes chunk i (16 B) of the line of session 8g+q
-        const uint32_t i = lane & 7u;
-        u32x16 addr;
-        u32x8 lim;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int src = (int)(lane & ~7u) | q;
-            const uint64_t a = __shfl((uint64_t)(uintptr_t)msg, src, 64) + 16u * i;
-            const uint32_t nb = __shfl(nblk, src, 64);
-            addr[2 * q] = (uint32_t)a;
-            addr[2 * q + 1] = (uint32_t)(a >> 32);
-            lim[q] = nb > (i >> 2) ? nb - (i >> 2) : 0u;      // store iff b + (i >= 4) < nb
-        }
+    if (ls.wmax) {
         const uint64_t s = (uint64_t)(uintptr_t)sinkp;
-        const u32x2 sink = {(uint32_t)s, (uint32_t)(s >> 32)};
-        crypt_lines_asm(st, P, Q, addr, lim, (uint64_t)(uintptr_t)msg + 256u, nblk, wmax, sink);
+        crypt_lines_asm(st, P, Q, ls, u32x2{(uint32_t)s, (uint32_t)(s >> 32)});
     }
-    uint4 *p = reinterpret_cast<uint4 *>(msg + 64u * nblk);
+    uint4 *p = reinterpret_cast<uint4 *>(msg + 64u * ls.nblk);
     uint32_t rem = len & 63u;
     while (rem >= 16u) {
         *p = xor16(S, st, *p);
@@ -819,10 +875,10 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
              uint32_t *__restrict__ err, uint8_t *__restrict__ sink)
 {
     // one LDS object: 64 KiB S-box image (+ 4 x 4 KiB store staging for the
-    // LDS-staged store paths: 80 KiB, so two workgroups fill the CU's 160 KiB).
-    constexpr bool kLdsStage = STAGED && ZRC4_STORE_PATH != 2;
-    constexpr bool kDpp = STAGED && ZRC4_STORE_PATH == 2;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsStage ? kSmemBytes : kGroupBytes + 16];
+    // LDS-staged store paths 0/1: 80 KiB, so two workgroups fill the CU's
+    // 160 KiB).  Path 2 (the default) runs throughput launches in
+    // crypt_stream_kernel instead.
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kSmemBytes : kGroupBytes + 16];
     uint8_t *S = smem;
 
     const uint32_t j = threadIdx.x;
@@ -860,18 +916,7 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     const uint32_t col = col_of(j);
     uint8_t *msg = payload + myoff;
     uint4 A[4];
-    const bool pre = !kDpp && active && mylen >= 64u && head_bytes(msg, mylen) == 0u;
-    u32x32 P, Q;
-    if constexpr (kDpp) {
-        // lines 0 and 1 of the message loop, issued ahead of the image fill
-        // (blocks past the session's end read the lane's sink slot)
-        const uint32_t h = head_bytes(msg, mylen);
-        const uint8_t *p = msg + h;
-        const uint32_t nb = (mylen - h) >> 6;
-        const uint8_t *sk = sink + (size_t)j * kSinkSlot;
-        preload_line(P, nb > 0 ? p : sk, nb > 1 ? p + 64 : sk + 64);
-        preload_line(Q, nb > 2 ? p + 128 : sk, nb > 3 ? p + 192 : sk + 64);
-    }
+    const bool pre = active && mylen >= 64u && head_bytes(msg, mylen) == 0u;
     if (whole) {
         if (!(ZRC4_ABLATE & 8)) {
         uint4 img[16];
@@ -904,9 +949,7 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         st.ya = (y << 8) | col;
         st.ta = col;
         st.x1 = col;
-        if constexpr (kDpp)
-            crypt_message_dpp(S, st, msg, mylen, P, Q, sink + (size_t)j * kSinkSlot);
-        else if constexpr (ZRC4_STORE_PATH == 1)
+        if constexpr (ZRC4_STORE_PATH == 1)
             crypt_message_lines(S, smem + kGroupBytes + (j >> 6) * kStageBytes, st, msg, mylen, A, pre);
         else
             crypt_message_staged(S, smem + kGroupBytes + (j >> 6) * kStageBytes, st, msg, mylen, A, pre);
@@ -931,6 +974,247 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         if (!(ZRC4_ABLATE & 16)) lds_to_image(arena + (size_t)g * kGroupBytes, S);
     } else if (active && mylen) {
         scatter_column(arena, slot, S, col);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// crypt_stream_kernel: the throughput-regime crypt (more groups than CUs),
+// persistent over groups.
+//
+// With one group per workgroup every workgroup of a round loads its 64 KiB
+// S-box image, runs, and stores the image at the same time, so the HBM idles
+// during the keystream and the LDS idles during the image bursts (the
+// ablation put the image I/O at 42 us of a 330 us cfg5 launch,
+// profiles/r01_ab_ablation_v7.log).  Here grid = 2 workgroups per CU and each
+// workgroup walks groups w, w + grid, ...; while group w's keystream runs, the
+// next group's image (16 x 16 B per lane, in VGPRs), its batch entries and --
+// once the message loop is done -- its first two payload lines are already in
+// flight, and the finished image goes back to HBM behind the next group's
+// work.  At a boundary only the LDS copies and three barriers remain.
+//   PF = range batch with first_slot % 256 == 0: every group is a whole,
+//        aligned image and is prefetched; otherwise (ids, unaligned range)
+//        each group decides whole/gather as crypt_kernel does, unprefetched.
+// ---------------------------------------------------------------------------
+struct EntryIn {
+    uint32_t len;    // 0 for idle lanes
+    uint32_t slot;   // ZRC4_INVALID for idle lanes
+    uint64_t off;
+    uint32_t xy;
+};
+
+__device__ __forceinline__ void load_entry(EntryIn &d, uint32_t w, const uint32_t *ids, uint32_t first_slot,
+                                           const uint64_t *off, const uint32_t *len, uint32_t n,
+                                           uint32_t capacity, uint32_t *err, const uint16_t *xy)
+{
+    const uint32_t e = w * kGroup + threadIdx.x;
+    const bool valid = e < n;
+    uint32_t slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
+    if (valid && slot >= capacity) {
+        latch_fault(err);
+        slot = ZRC4_INVALID;
+    }
+    // No load here depends on another's value (the range path's slot is
+    // arithmetic), so prefetching a group never makes the compiler wait.
+    d.len = (slot != ZRC4_INVALID) ? len[e] : 0u;
+    d.off = (slot != ZRC4_INVALID) ? off[e] : 0u;
+    d.slot = slot;
+    d.xy = (slot != ZRC4_INVALID) ? xy[slot] : 0u;
+}
+
+
+// Next group's batch entries and S-box image, issued from asm so the compiler
+// neither waits for them nor counts them: it would otherwise drain them at
+// its next wait for anything younger (in-order vmcnt).  P/Q are passed
+// through so the compiler's wait for this group's first lines lands BEFORE
+// these loads.  Consumers wait explicitly:
+//   entries  "s_waitcnt vmcnt(16)" (the 16 image loads are younger);
+//   image    "s_waitcnt vmcnt(32)" (the next lines' 16 loads and this image's
+//            16 stores are younger).
+__device__ __forceinline__ void prefetch_group(u32x32 &P, u32x32 &Q, u32x32 &ilo, u32x32 &ihi,
+                                               uint32_t &rlen, uint64_t &roff, uint32_t &rxy,
+                                               const uint32_t *alen, const uint64_t *aoff,
+                                               const uint16_t *axy, const uint8_t *ibase)
+{
+    uint32_t vo;
+    asm volatile(
+        "global_load_dword %[rlen], %[alen], off\n\t"
+        "global_load_dwordx2 %[roff], %[aoff], off\n\t"
+        "global_load_ushort %[rxy], %[axy], off\n\t"
+        "v_lshlrev_b32 %[vo], 4, %[j]\n\t"
+        "global_load_dwordx4 v[160:163], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[164:167], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[168:171], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[172:175], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[176:179], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[180:183], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[184:187], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[188:191], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[192:195], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[196:199], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[200:203], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[204:207], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[208:211], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[212:215], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[216:219], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[220:223], %[vo], %[ib]\n\t"
+        : "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[160:191]}"(ilo), "=&{v[192:223]}"(ihi),
+          [rlen] "=&v"(rlen), [roff] "=&v"(roff), [rxy] "=&v"(rxy), [vo] "=&v"(vo)
+        : [alen] "v"(alen), [aoff] "v"(aoff), [axy] "v"(axy), [ib] "s"(ibase), [j] "v"(threadIdx.x)
+        : "memory");
+}
+
+template <bool PF>
+__global__ void __launch_bounds__(256, 2)
+crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
+                    const uint32_t *__restrict__ ids, uint32_t first_slot,
+                    uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
+                    const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
+                    uint32_t *__restrict__ err, uint8_t *__restrict__ sink)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kGroupBytes + 16];
+    uint8_t *S = smem;
+    const uint32_t j = threadIdx.x;
+    const uint32_t col = col_of(j);
+    const uint32_t nwg = (n + kGroup - 1) / kGroup;
+    uint8_t *sk = sink + (size_t)j * kSinkSlot;
+
+    uint32_t w = blockIdx.x;
+    EntryIn cur;
+    load_entry(cur, w, ids, first_slot, off, len, n, capacity, err, xy);
+    u32x32 ilo, ihi;                          // PF: this group's image, 16 x 16 B per lane
+    if constexpr (PF) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(arena + (size_t)((first_slot >> 8) + w) * kGroupBytes);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const u32x4 a = src[i * 256 + j], b = src[(i + 8) * 256 + j];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                ilo[4 * i + d] = a[d];
+                ihi[4 * i + d] = b[d];
+            }
+        }
+    }
+    LineSetup ls;
+    line_setup(ls, payload + cur.off, cur.len);
+    u32x32 P, Q;
+    preload_lines(P, Q, ls, sk);
+    // Retire the prologue's loads here, once: inside the loop the compiler's
+    // waitcnt analysis merges the first iteration with the back edge, and a
+    // value still pending from the prologue would put a vmcnt(0) -- draining
+    // the asm prefetch -- into every iteration.
+    asm volatile("" : "+v"(cur.len), "+v"(cur.off), "+v"(cur.xy), "+{v[40:71]}"(P), "+{v[72:103]}"(Q),
+                 "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi));
+
+    for (;;) {
+        // ---- this group's S-boxes into LDS
+        bool whole;
+        uint32_t g;
+        const bool active = cur.slot != ZRC4_INVALID;
+        if constexpr (PF) {
+            whole = true;
+            g = (first_slot >> 8) + w;
+            asm volatile("s_waitcnt vmcnt(32)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
+            u32x4 *dst = reinterpret_cast<u32x4 *>(S);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                dst[i * 256 + j] = u32x4{ilo[4 * i], ilo[4 * i + 1], ilo[4 * i + 2], ilo[4 * i + 3]};
+                dst[(i + 8) * 256 + j] = u32x4{ihi[4 * i], ihi[4 * i + 1], ihi[4 * i + 2], ihi[4 * i + 3]};
+            }
+            __syncthreads();
+        } else {
+            if (!ids) {
+                whole = (first_slot & 255u) == 0u;
+                g = (first_slot >> 8) + w;
+            } else {
+                const uint32_t first = ids[w * kGroup];
+                g = first >> 8;
+                whole = __syncthreads_and(active && cur.slot == ((first & ~255u) + j) && (first & 255u) == 0u);
+            }
+            if (whole) {
+                image_to_lds(S, arena + (size_t)g * kGroupBytes);
+                __syncthreads();
+            } else if (active && cur.len) {
+                gather_column(S, col, arena, cur.slot);
+            }
+        }
+
+        // ---- next group's entries and image, in flight during the keystream (PF)
+        const uint32_t wn = w + gridDim.x;
+        const bool more = wn < nwg;
+        uint32_t rlen = 0, rxy = 0;
+        uint64_t roff = 0;
+        uint32_t en = 0;
+        // This group's first lines are needed now (compiler wait: vmcnt(16),
+        // the previous image's stores are younger); past this point they are
+        // asm-defined, so nothing the compiler tracks is pending at the loop.
+        asm volatile("" : "+{v[40:71]}"(P), "+{v[72:103]}"(Q));
+        if constexpr (PF) {
+            if (more) {
+                en = wn * kGroup + j;
+                const uint32_t ec = en < n ? en : n - 1u;          // in-bounds address for idle lanes
+                prefetch_group(P, Q, ilo, ihi, rlen, roff, rxy, len + ec, off + ec, xy + first_slot + ec,
+                               arena + (size_t)((first_slot >> 8) + wn) * kGroupBytes);
+            }
+        }
+
+        // ---- keystream over this group's messages
+        {
+            const uint32_t x = cur.xy & 255u, y = (cur.xy >> 8) & 255u;
+            Rc4Lane st;
+            st.col = col;
+            st.x0 = (((x + 1u) & 255u) << 8) | col;
+            st.a0 = S[st.x0];
+            st.ya = (y << 8) | col;
+            st.ta = col;
+            st.x1 = col;
+            crypt_message_dpp(S, st, payload + cur.off, cur.len, P, Q, ls, sk);
+            if (active && cur.len)
+                xy[cur.slot] = (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
+        }
+
+        EntryIn nxt = {0u, ZRC4_INVALID, 0u, 0u};
+        if (more) {
+            if constexpr (PF) {
+                asm volatile("s_waitcnt vmcnt(16)" : "+v"(rlen), "+v"(roff), "+v"(rxy) :: "memory");
+                const bool v = en < n;
+                nxt.len = v ? rlen : 0u;
+                nxt.off = v ? roff : 0u;
+                nxt.slot = v ? first_slot + en : ZRC4_INVALID;
+                nxt.xy = v ? rxy : 0u;
+            } else {
+                load_entry(nxt, wn, ids, first_slot, off, len, n, capacity, err, xy);
+            }
+            // the loop's last two halves issue no loads, so P/Q are free again
+            line_setup(ls, payload + nxt.off, nxt.len);
+            preload_lines(P, Q, ls, sk);
+        }
+
+        // ---- this group's state back to HBM
+        if (whole) {
+            __syncthreads();
+            lds_to_image(arena + (size_t)g * kGroupBytes, S);
+        } else if (active && cur.len) {
+            scatter_column(arena, cur.slot, S, col);
+        }
+        if (!more) break;
+        __syncthreads();      // every wave has read this image out of LDS before the next fill
+        cur = nxt;
+        w = wn;
     }
 }
 
