@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--footprint-mib", type=int, default=640)
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--ksa", action="store_true", help="also time zrc4_ksa_range per variant")
+    ap.add_argument("--segment", action="store_true",
+                    help="time each round's launches as one back-to-back segment (per-launch average)")
     ap.add_argument("--no-check", action="store_true", help="timing-only ablation builds (outputs differ)")
     args = ap.parse_args()
 
@@ -129,20 +131,30 @@ def main():
         for r in range(args.rounds):
             for (name, lib), h in zip(libs, ctxs):
                 evs = []
+                if args.segment:               # back-to-back launches, like bench.py (kernel boundaries included)
+                    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s0.record(stream)
                 for i in range(args.launches):
                     b = step % R
                     step += 1
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(stream)
+                    if not args.segment:
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record(stream)
                     rc = lib.zrc4_crypt_range(h, b * S, C.c_void_p(pay.data_ptr()),
                                               C.c_void_p(off.data_ptr() + 8 * b * S),
                                               C.c_void_p(ln.data_ptr() + 4 * b * S), S, st)
-                    e1.record(stream)
-                    evs.append((e0, e1))
+                    if not args.segment:
+                        e1.record(stream)
+                        evs.append((e0, e1))
                     if rc:
                         raise SystemExit(f"{name}: crypt failed {rc}")
+                if args.segment:
+                    s1.record(stream)
                 torch.cuda.synchronize()
-                times[name].extend(a.elapsed_time(b_) * 1e3 for a, b_ in evs)
+                if args.segment:
+                    times[name].append(s0.elapsed_time(s1) * 1e3 / args.launches)
+                else:
+                    times[name].extend(a.elapsed_time(b_) * 1e3 for a, b_ in evs)
         B = 2 * S * L + 516 * S
         report[wl] = {name: {"median_us": round(statistics.median(t), 2), "min_us": round(min(t), 2),
                              "hbm_frac": round(B / (statistics.median(t) * 1e-6) / 8e12, 4)}

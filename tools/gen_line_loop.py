@@ -157,7 +157,7 @@ def half(name: str, cur: int) -> str:
         w(q(f"v_cmp_gt_u32_e64 %[msk], v{LIM_BASE + qq}, %[sb]"))
         w(q(f"v_cndmask_b32_e64 v{sa}, v{SINK}, v{a}, %[msk]"))
         w(q(f"v_cndmask_b32_e64 v{sa + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
-        w(q(f"global_store_dwordx4 v[{sa}:{sa + 1}], v[{final[qq]}:{final[qq] + 3}], off"))
+        w(f'"global_store_dwordx4 v[{sa}:{sa + 1}], v[{final[qq]}:{final[qq] + 3}], off" ZRC4_LL_STP "\\n\\t"')
     for qq in range(8):
         a = ADDR_BASE + 2 * qq
         w(q(f"v_lshl_add_u64 v[{a}:{a + 1}], 8, 4, v[{a}:{a + 1}]"))     # += 8 << 4 (shift must be 0..4)
@@ -170,13 +170,13 @@ def half(name: str, cur: int) -> str:
     w(q(f"v_cndmask_b32_e64 v{LA}, v{SINK}, %[palo], %[msk]"))
     w(q(f"v_cndmask_b32_e64 v{LA + 1}, v{SINK + 1}, %[pahi], %[msk]"))
     for d in range(4):
-        w(q(f"global_load_dwordx4 v[{cur + 4 * d}:{cur + 4 * d + 3}], v[{LA}:{LA + 1}], off offset:{16 * d}"))
+        w(f'"global_load_dwordx4 v[{cur + 4 * d}:{cur + 4 * d + 3}], v[{LA}:{LA + 1}], off offset:{16 * d}" ZRC4_LDP "\\n\\t"')
     w(q("s_add_u32 %[s1], %[sb], 5"))
     w(q("v_cmp_lt_u32_e64 %[msk], %[s1], %[nblk]"))
     w(q(f"v_cndmask_b32_e64 v{LB}, v{SINK}, %[palo], %[msk]"))
     w(q(f"v_cndmask_b32_e64 v{LB + 1}, v{SINK + 1}, %[pahi], %[msk]"))
     for d in range(4):
-        w(q(f"global_load_dwordx4 v[{cur + 16 + 4 * d}:{cur + 16 + 4 * d + 3}], v[{LB}:{LB + 1}], off offset:{64 + 16 * d}"))
+        w(f'"global_load_dwordx4 v[{cur + 16 + 4 * d}:{cur + 16 + 4 * d + 3}], v[{LB}:{LB + 1}], off offset:{64 + 16 * d}" ZRC4_LDP "\\n\\t"')
     w(q("v_add_co_u32_e32 %[palo], vcc, 0x80, %[palo]"))
     w(q("v_addc_co_u32_e32 %[pahi], vcc, 0, %[pahi], vcc"))
     w(q(f"LL_{name}L_%=:"))
@@ -232,7 +232,7 @@ def half_coalesced(name: str, cur: int) -> str:
         w(q(f"v_cmp_gt_u32_e64 %[msk], v{LIM_BASE + qq}, %[sb]"))
         w(q(f"v_cndmask_b32_e64 v{sa}, v{SINK}, v{a}, %[msk]"))
         w(q(f"v_cndmask_b32_e64 v{sa + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
-        w(q(f"global_store_dwordx4 v[{sa}:{sa + 1}], v[{smap[qq]}:{smap[qq] + 3}], off"))
+        w(f'"global_store_dwordx4 v[{sa}:{sa + 1}], v[{smap[qq]}:{smap[qq] + 3}], off" ZRC4_LL_STP "\\n\\t"')
     for qq in range(8):
         a = ADDR_BASE + 2 * qq
         w(q(f"v_lshl_add_u64 v[{a}:{a + 1}], 8, 4, v[{a}:{a + 1}]"))     # += 8 << 4 (shift must be 0..4)
@@ -246,7 +246,7 @@ def half_coalesced(name: str, cur: int) -> str:
         w(q(f"v_cmp_gt_u32_e64 %[msk], v{LIM_BASE + qq}, %[s1]"))
         w(q(f"v_cndmask_b32_e64 v{la}, v{SINK}, v{a}, %[msk]"))
         w(q(f"v_cndmask_b32_e64 v{la + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
-        w(q(f"global_load_dwordx4 v[{cur + 4 * qq}:{cur + 4 * qq + 3}], v[{la}:{la + 1}], off offset:128"))
+        w(f'"global_load_dwordx4 v[{cur + 4 * qq}:{cur + 4 * qq + 3}], v[{la}:{la + 1}], off offset:128" ZRC4_LDP "\\n\\t"')
     w(q(f"LC_{name}L_%=:"))
     w(q("s_add_u32 %[sb], %[sb], 2"))
     w(q("s_cmp_ge_u32 %[sb], %[wmax]"))

@@ -101,7 +101,12 @@ int launch_crypt(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, uint8_t 
                            c->err, c->sink);
     else
 #endif
-        hipLaunchKernelGGL(zrc4::crypt_kernel<false>, dim3(grid), dim3(zrc4::kGroup), 0, s,
+    if (!ids)
+        hipLaunchKernelGGL((zrc4::crypt_kernel<false, true>), dim3(grid), dim3(zrc4::kGroup), 0, s,
+                           c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
+                           c->err, c->sink);
+    else
+        hipLaunchKernelGGL((zrc4::crypt_kernel<false, false>), dim3(grid), dim3(zrc4::kGroup), 0, s,
                            c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
                            c->err, c->sink);
     return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;

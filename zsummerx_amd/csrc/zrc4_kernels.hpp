@@ -68,6 +68,16 @@ __device__ __forceinline__ void lds_to_image(uint8_t *img, const uint8_t *lds)
     for (int i = 0; i < 16; ++i) dst[i * 256 + threadIdx.x] = src[i * 256 + threadIdx.x];
 }
 
+// Same copy with nontemporal (nt) stores: the image is not read again in
+// this launch, so it need not compete for L2 (A/B knob ZRC4_IMG_NT).
+__device__ __forceinline__ void lds_to_image_nt(uint8_t *img, const uint8_t *lds)
+{
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(lds);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(img);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) __builtin_nontemporal_store(src[i * 256 + threadIdx.x], &dst[i * 256 + threadIdx.x]);
+}
+
 __device__ __forceinline__ void gather_column(uint8_t *lds, uint32_t col,
                                               const uint8_t *arena, uint32_t slot)
 {
@@ -268,6 +278,49 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
 //     restored on exit.  Lanes keep their own pointer and RC4 state.
 // On entry A holds block 0 (landed), nblk >= 1 for every active lane.
 // ---------------------------------------------------------------------------
+// Cache policy of the payload stores / loads issued from asm.
+//   ZRC4_STP_MODE (direct path) / ZRC4_LL_STP_MODE (throughput line loop):
+//     0 plain, 1 sc1, 2 nt, 3 sc0 sc1;   ZRC4_LDP_MODE (both): 0 plain, 1 nt, 2 sc1
+// Measured back to back (profiles/r01_ab_cache_policy.log): nt stores take
+// cfg5 from 306.6 to 291.6 us (the streamed lines stop competing for L2) but
+// cost cfg3 +2.7 %; sc1 / sc0 sc1 stores and nt loads are slower.
+#ifndef ZRC4_STP_MODE
+#define ZRC4_STP_MODE 0
+#endif
+#ifndef ZRC4_IMG_NT
+#define ZRC4_IMG_NT 0
+#endif
+#ifndef ZRC4_LL_STP_MODE
+#define ZRC4_LL_STP_MODE 2
+#endif
+#if ZRC4_LL_STP_MODE == 1
+#define ZRC4_LL_STP " sc1"
+#elif ZRC4_LL_STP_MODE == 2
+#define ZRC4_LL_STP " nt"
+#elif ZRC4_LL_STP_MODE == 3
+#define ZRC4_LL_STP " sc0 sc1"
+#else
+#define ZRC4_LL_STP ""
+#endif
+#ifndef ZRC4_LDP_MODE
+#define ZRC4_LDP_MODE 0
+#endif
+#if ZRC4_STP_MODE == 1
+#define ZRC4_STP " sc1"
+#elif ZRC4_STP_MODE == 2
+#define ZRC4_STP " nt"
+#elif ZRC4_STP_MODE == 3
+#define ZRC4_STP " sc0 sc1"
+#else
+#define ZRC4_STP ""
+#endif
+#if ZRC4_LDP_MODE == 1
+#define ZRC4_LDP " nt"
+#elif ZRC4_LDP_MODE == 2
+#define ZRC4_LDP " sc1"
+#else
+#define ZRC4_LDP ""
+#endif
 #define ZL_XOR(R, SEL, K)                                                                        \
     "v_xor_b32_sdwa " #R ", " #R ", %[" #K "] dst_sel:" #SEL                                     \
     " dst_unused:UNUSED_PRESERVE src0_sel:" #SEL " src1_sel:BYTE_0\n\t"
@@ -298,17 +351,17 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
     "s_add_u32 %[i1], %[i], 1\n\t"                                                               \
     "v_cmp_lt_u32_e32 vcc, %[i1], %[nblk]\n\t"                                                   \
     "s_and_saveexec_b64 %[tmp], vcc\n\t"                                                         \
-    "global_load_dwordx4 " ZL_B0 ", %[pa], off offset:64\n\t"                                    \
-    "global_load_dwordx4 " ZL_B1 ", %[pa], off offset:80\n\t"                                    \
-    "global_load_dwordx4 " ZL_B2 ", %[pa], off offset:96\n\t"                                    \
-    "global_load_dwordx4 " ZL_B3 ", %[pa], off offset:112\n\t"                                   \
+    "global_load_dwordx4 " ZL_B0 ", %[pa], off offset:64" ZRC4_LDP "\n\t"                                    \
+    "global_load_dwordx4 " ZL_B1 ", %[pa], off offset:80" ZRC4_LDP "\n\t"                                    \
+    "global_load_dwordx4 " ZL_B2 ", %[pa], off offset:96" ZRC4_LDP "\n\t"                                    \
+    "global_load_dwordx4 " ZL_B3 ", %[pa], off offset:112" ZRC4_LDP "\n\t"                                   \
     "s_mov_b64 exec, %[tmp]\n\t"                                                                 \
     "s_waitcnt vmcnt(8)\n\t"                                                                     \
     ZL_BLOCK(v40, v41, v42, v43, v44, v45, v46, v47, v48, v49, v50, v51, v52, v53, v54, v55)    \
-    "global_store_dwordx4 %[pa], " ZL_A0 ", off\n\t"                                             \
-    "global_store_dwordx4 %[pa], " ZL_A1 ", off offset:16\n\t"                                   \
-    "global_store_dwordx4 %[pa], " ZL_A2 ", off offset:32\n\t"                                   \
-    "global_store_dwordx4 %[pa], " ZL_A3 ", off offset:48\n\t"                                   \
+    "global_store_dwordx4 %[pa], " ZL_A0 ", off" ZRC4_STP "\n\t"                                             \
+    "global_store_dwordx4 %[pa], " ZL_A1 ", off offset:16" ZRC4_STP "\n\t"                                   \
+    "global_store_dwordx4 %[pa], " ZL_A2 ", off offset:32" ZRC4_STP "\n\t"                                   \
+    "global_store_dwordx4 %[pa], " ZL_A3 ", off offset:48" ZRC4_STP "\n\t"                                   \
     "v_lshl_add_u64 %[pa], %[pa], 0, 64\n\t"                                                     \
     "s_add_u32 %[i], %[i], 1\n\t"
 #define ZL_HALF_B                                                                                \
@@ -318,17 +371,17 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
     "s_add_u32 %[i1], %[i], 1\n\t"                                                               \
     "v_cmp_lt_u32_e32 vcc, %[i1], %[nblk]\n\t"                                                   \
     "s_and_saveexec_b64 %[tmp], vcc\n\t"                                                         \
-    "global_load_dwordx4 " ZL_A0 ", %[pa], off offset:64\n\t"                                    \
-    "global_load_dwordx4 " ZL_A1 ", %[pa], off offset:80\n\t"                                    \
-    "global_load_dwordx4 " ZL_A2 ", %[pa], off offset:96\n\t"                                    \
-    "global_load_dwordx4 " ZL_A3 ", %[pa], off offset:112\n\t"                                   \
+    "global_load_dwordx4 " ZL_A0 ", %[pa], off offset:64" ZRC4_LDP "\n\t"                                    \
+    "global_load_dwordx4 " ZL_A1 ", %[pa], off offset:80" ZRC4_LDP "\n\t"                                    \
+    "global_load_dwordx4 " ZL_A2 ", %[pa], off offset:96" ZRC4_LDP "\n\t"                                    \
+    "global_load_dwordx4 " ZL_A3 ", %[pa], off offset:112" ZRC4_LDP "\n\t"                                   \
     "s_mov_b64 exec, %[tmp]\n\t"                                                                 \
     "s_waitcnt vmcnt(8)\n\t"                                                                     \
     ZL_BLOCK(v56, v57, v58, v59, v60, v61, v62, v63, v64, v65, v66, v67, v68, v69, v70, v71)    \
-    "global_store_dwordx4 %[pa], " ZL_B0 ", off\n\t"                                             \
-    "global_store_dwordx4 %[pa], " ZL_B1 ", off offset:16\n\t"                                   \
-    "global_store_dwordx4 %[pa], " ZL_B2 ", off offset:32\n\t"                                   \
-    "global_store_dwordx4 %[pa], " ZL_B3 ", off offset:48\n\t"                                   \
+    "global_store_dwordx4 %[pa], " ZL_B0 ", off" ZRC4_STP "\n\t"                                             \
+    "global_store_dwordx4 %[pa], " ZL_B1 ", off offset:16" ZRC4_STP "\n\t"                                   \
+    "global_store_dwordx4 %[pa], " ZL_B2 ", off offset:32" ZRC4_STP "\n\t"                                   \
+    "global_store_dwordx4 %[pa], " ZL_B3 ", off offset:48" ZRC4_STP "\n\t"                                   \
     "v_lshl_add_u64 %[pa], %[pa], 0, 64\n\t"                                                     \
     "s_add_u32 %[i], %[i], 1\n\t"
 
@@ -735,31 +788,36 @@ __device__ __forceinline__ void preload_line(u32x32 &v, const uint8_t *b0, const
 // depend on the S-boxes, so it can be computed (and the first two lines
 // loaded) before the group's S-box image is in LDS.
 //   p      the message after its unaligned head bytes, nblk its 64-byte blocks
-//   addr/lim  store (and, with line loads, load) role: lane 8g+i moves chunk
-//          i of the line of session 8g+q; lim_q = blocks of that session
-//          minus (i >= 4), so chunk i of the line at block b exists iff b < lim_q
+// The line roles (line_roles) are derived from these right where they are
+// needed: holding 24 more VGPRs across a group boundary spilled the
+// persistent kernel.
 struct LineSetup {
-    u32x16 addr;
-    u32x8 lim;
     uint64_t p;
     uint32_t nblk, wmax;
 };
 
 __device__ __forceinline__ void line_setup(LineSetup &ls, const uint8_t *msg, uint32_t len)
 {
-    const uint32_t lane = threadIdx.x & 63u, i = lane & 7u;
     const uint32_t h = head_bytes(msg, len);
     ls.p = (uint64_t)(uintptr_t)(msg + h);
     ls.nblk = (len - h) >> 6;
     ls.wmax = __builtin_amdgcn_readfirstlane(wave_max(ls.nblk));
+}
+
+// Store (and, with line loads, load) role: lane 8g+i moves chunk i of the
+// line of session 8g+q at addr_q; lim_q = blocks of that session minus
+// (i >= 4), so chunk i of the line at block b exists iff b < lim_q.
+__device__ __forceinline__ void line_roles(u32x16 &addr, u32x8 &lim, const LineSetup &ls)
+{
+    const uint32_t lane = threadIdx.x & 63u, i = lane & 7u;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int src = (int)(lane & ~7u) | q;
         const uint64_t a = __shfl(ls.p, src, 64) + 16u * i;
         const uint32_t nb = __shfl(ls.nblk, src, 64);
-        ls.addr[2 * q] = (uint32_t)a;
-        ls.addr[2 * q + 1] = (uint32_t)(a >> 32);
-        ls.lim[q] = nb > (i >> 2) ? nb - (i >> 2) : 0u;
+        addr[2 * q] = (uint32_t)a;
+        addr[2 * q + 1] = (uint32_t)(a >> 32);
+        lim[q] = nb > (i >> 2) ? nb - (i >> 2) : 0u;
     }
 }
 
@@ -768,12 +826,15 @@ __device__ __forceinline__ void preload_lines(u32x32 &P, u32x32 &Q, const LineSe
 {
 #if ZRC4_LINE_LOADS
     // tuple q = chunk i of the line of session 8g+q
+    u32x16 addr;
+    u32x8 lim;
+    line_roles(addr, lim, ls);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const uint8_t *a = reinterpret_cast<const uint8_t *>(
-            (uintptr_t)(((uint64_t)ls.addr[2 * q + 1] << 32) | ls.addr[2 * q]));
-        const u32x4 t0 = *reinterpret_cast<const u32x4 *>(ls.lim[q] > 0u ? a : sk);
-        const u32x4 t1 = *reinterpret_cast<const u32x4 *>(ls.lim[q] > 2u ? a + 128 : sk);
+            (uintptr_t)(((uint64_t)addr[2 * q + 1] << 32) | addr[2 * q]));
+        const u32x4 t0 = *reinterpret_cast<const u32x4 *>(lim[q] > 0u ? a : sk);
+        const u32x4 t1 = *reinterpret_cast<const u32x4 *>(lim[q] > 2u ? a + 128 : sk);
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
             P[4 * q + d] = t0[d];
@@ -789,11 +850,11 @@ __device__ __forceinline__ void preload_lines(u32x32 &P, u32x32 &Q, const LineSe
 #endif
 }
 
-__device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls, u32x2 sink)
+__device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls,
+                                                u32x16 &addr, const u32x8 &lim, u32x2 sink)
 {
     u32x16 X;
     u32x8 T;
-    u32x16 addr = ls.addr;
     uint32_t b, k0, k1, a1s, sb, s1;
     const uint64_t pa = ls.p + 256u;                 // per-lane loads: blocks 4, 5 next
     uint32_t palo = (uint32_t)pa, pahi = (uint32_t)(pa >> 32);
@@ -819,7 +880,7 @@ __device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &
           [full] "=&s"(full), [msk] "=&s"(msk),
           "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
           "=&{v[144:151]}"(T)
-        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), "{v[136:143]}"(ls.lim), "{v[152:153]}"(sink)
+        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), "{v[136:143]}"(lim), "{v[152:153]}"(sink)
         : "memory", "vcc", "scc");
 }
 
@@ -833,8 +894,11 @@ __device__ __forceinline__ void crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8
     msg += head;
     len -= head;
     if (ls.wmax) {
+        u32x16 addr;
+        u32x8 lim;
+        line_roles(addr, lim, ls);
         const uint64_t s = (uint64_t)(uintptr_t)sinkp;
-        crypt_lines_asm(st, P, Q, ls, u32x2{(uint32_t)s, (uint32_t)(s >> 32)});
+        crypt_lines_asm(st, P, Q, ls, addr, lim, u32x2{(uint32_t)s, (uint32_t)(s >> 32)});
     }
     uint4 *p = reinterpret_cast<uint4 *>(msg + 64u * ls.nblk);
     uint32_t rem = len & 63u;
@@ -859,6 +923,49 @@ __device__ __forceinline__ void crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8
 //   ids != NULL : whole iff the 256 ids are exactly g*256 .. g*256+255
 #define ZRC4_INVALID 0xFFFFFFFFu
 
+// One group's 64 KiB S-box image, 16 x 16 B per lane into v160..v223, issued
+// from asm and NOT waited for (the caller waits with a counted vmcnt).
+__device__ __forceinline__ void issue_image_asm(u32x32 &ilo, u32x32 &ihi, const uint8_t *ibase)
+{
+    uint32_t vo;
+    asm volatile(
+        "v_lshlrev_b32 %[vo], 4, %[j]\n\t"
+        "global_load_dwordx4 v[160:163], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[164:167], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[168:171], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[172:175], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[176:179], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[180:183], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[184:187], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[188:191], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[192:195], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[196:199], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[200:203], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[204:207], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[208:211], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[212:215], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[216:219], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[220:223], %[vo], %[ib]\n\t"
+        : "=&{v[160:191]}"(ilo), "=&{v[192:223]}"(ihi), [vo] "=&v"(vo)
+        : [ib] "s"(ibase), [j] "v"(threadIdx.x)
+        : "memory");
+}
+
 // ---------------------------------------------------------------------------
 // crypt_kernel: batched RC4Encryption::encryption.
 // grid = ceil(n / 256) workgroups of 256 threads; workgroup w handles batch
@@ -866,7 +973,14 @@ __device__ __forceinline__ void crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8
 // first (group image, len/off/xy, the first payload block) so it costs about
 // two HBM round trips instead of a dependent chain of them.
 // ---------------------------------------------------------------------------
-template <bool STAGED>
+//
+// RANGE (ids == NULL, the hook engine's and the bench's batches): the slot is
+// arithmetic and the host has checked first_slot + n <= capacity, so the
+// group image, len/off and x/y are issued together with no load waiting on
+// another (one HBM round trip instead of two); only the first payload block
+// waits for off/len.
+// ---------------------------------------------------------------------------
+template <bool STAGED, bool RANGE = false>
 __global__ void __launch_bounds__(256, 2)
 crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
              const uint32_t *__restrict__ ids, uint32_t first_slot,
@@ -884,20 +998,33 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     const uint32_t j = threadIdx.x;
     const uint32_t e = blockIdx.x * kGroup + j;
     const bool valid = e < n;
+    uint4 img[16];
+    u32x32 ilo, ihi;
+    if constexpr (RANGE) {
+        // Issued from asm, first: hipcc otherwise sinks these loads below its
+        // wait for len/off.  Group (first_slot >> 8) + w lies inside the arena
+        // even when first_slot is unaligned and the image goes unused.
+        issue_image_asm(ilo, ihi, arena + (size_t)((first_slot >> 8) + blockIdx.x) * kGroupBytes);
+    }
     const uint32_t mylen0 = valid ? len[e] : 0u;
     const uint64_t myoff = valid ? off[e] : 0u;
-    uint32_t slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
-    if (valid && slot >= capacity) {
-        latch_fault(err);
-        slot = ZRC4_INVALID;
+    uint32_t slot;
+    if constexpr (RANGE) {
+        slot = valid ? first_slot + e : ZRC4_INVALID;
+    } else {
+        slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
+        if (valid && slot >= capacity) {
+            latch_fault(err);
+            slot = ZRC4_INVALID;
+        }
     }
     const bool active = slot != ZRC4_INVALID;
     const uint32_t mylen = active ? mylen0 : 0u;
-    const uint16_t sxy = (active && mylen) ? xy[slot] : (uint16_t)0;
+    const uint16_t sxy = (RANGE ? active : (active && mylen)) ? xy[slot] : (uint16_t)0;
 
     bool whole;
     uint32_t g;
-    if (!ids) {
+    if (RANGE || !ids) {
         whole = (first_slot & 255u) == 0u;
         g = (first_slot >> 8) + blockIdx.x;
     } else {
@@ -917,12 +1044,25 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     uint8_t *msg = payload + myoff;
     uint4 A[4];
     const bool pre = active && mylen >= 64u && head_bytes(msg, mylen) == 0u;
+    if constexpr (RANGE) {
+        // The image was issued before len, off and x/y (3 loads).  Waited
+        // on every path (the registers must not be reused while it is in
+        // flight); the first payload block is issued after this wait, so its
+        // round trip overlaps the LDS fill.
+        asm volatile("s_waitcnt vmcnt(3)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            img[i] = make_uint4(ilo[4 * i], ilo[4 * i + 1], ilo[4 * i + 2], ilo[4 * i + 3]);
+            img[i + 8] = make_uint4(ihi[4 * i], ihi[4 * i + 1], ihi[4 * i + 2], ihi[4 * i + 3]);
+        }
+    }
     if (whole) {
         if (!(ZRC4_ABLATE & 8)) {
-        uint4 img[16];
-        const uint4 *src = reinterpret_cast<const uint4 *>(arena + (size_t)g * kGroupBytes);
+        if constexpr (!RANGE) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(arena + (size_t)g * kGroupBytes);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) img[i] = src[i * 256 + j];
+            for (int i = 0; i < 16; ++i) img[i] = src[i * 256 + j];
+        }
         if (pre) load64(A, reinterpret_cast<const uint4 *>(msg));
         uint4 *dst = reinterpret_cast<uint4 *>(S);
 #pragma unroll
@@ -1207,7 +1347,10 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         // ---- this group's state back to HBM
         if (whole) {
             __syncthreads();
-            lds_to_image(arena + (size_t)g * kGroupBytes, S);
+            if (ZRC4_IMG_NT)
+                lds_to_image_nt(arena + (size_t)g * kGroupBytes, S);
+            else
+                lds_to_image(arena + (size_t)g * kGroupBytes, S);
         } else if (active && cur.len) {
             scatter_column(arena, cur.slot, S, col);
         }
