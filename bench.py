@@ -11,7 +11,9 @@ of the chosen workload:
 
 Multi-GPU: one process per GPU (torchrun), sessions shard across ranks with no
 collective on the data path; each rank runs the same per-GPU
-batch over its own global session ids -> "scaling": "weak".  torch.distributed
+batch over its own global session ids -> "scaling": "weak"; with --strong the
+workload's sessions are the whole job and ranks split them (BASELINE
+configs[4]: --workload cfg5 --strong).  torch.distributed
 is used only for the start/stop barrier and the max-over-ranks time.
 
 HBM honesty: each rank rotates over R distinct batches (distinct sessions,
@@ -59,6 +61,14 @@ def dist_env():
 def algorithmic_bytes(S: int, L: int) -> int:
     """B = 2*sum(L) + 516*S  (payload read+write + state load+store)."""
     return 2 * S * L + STATE_BYTES * S
+
+
+def per_rank_sessions(S_job: int, ws: int) -> int:
+    """Strong scaling: rank r owns sessions [r*S, (r+1)*S) of the job (whole
+    256-session groups; every BASELINE total divides evenly at 1/2/4/8)."""
+    if S_job % (256 * ws):
+        raise SystemExit(f"--strong: {S_job} sessions do not split into whole groups over {ws} ranks")
+    return S_job // ws
 
 
 def rotation_batches(S: int, L: int, footprint_mib: int) -> int:
@@ -159,7 +169,10 @@ def run_bench(args, ws, rank, local, backend="nccl", make_runner=None):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    S, L = CONFIG_SHAPES[args.workload]
+    S_job, L = CONFIG_SHAPES[args.workload]
+    # --strong: the workload's sessions are the WHOLE job (BASELINE configs[4]:
+    # 524 288 sessions sharded across the GPUs); otherwise every rank runs it
+    S = per_rank_sessions(S_job, ws) if args.strong else S_job
     R = rotation_batches(S, L, args.footprint_mib) if args.footprint_mib > 0 else 1
     if make_runner is None:
         runner = GpuRunner(torch, local, S, L, R, shard_first(rank, R, S))
@@ -196,7 +209,7 @@ def run_bench(args, ws, rank, local, backend="nccl", make_runner=None):
 
     res = None
     if rank == 0:
-        total_payload = ws * args.steps * S * L
+        total_payload = (args.steps * S_job * L) if args.strong else (ws * args.steps * S * L)
         res = build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload)
         # per-GPU achieved B/t separates a latency bound from a scaling bug
         B = algorithmic_bytes(S, L)
@@ -242,13 +255,17 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
         "warmup": args.warmup,
         "ms_per_step": round(tmax / args.steps * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (mt19937_64 keys seed 1, payload seed 42, pre-advance (sid*37)%1000)",
-        "config": {"workload": f"{args.workload}: {CONFIG_TEXT[args.workload]}",
+        "config": {"workload": (f"{args.workload}: {S * ws} sessions x {L} B job total, {S} per GPU "
+                                f"(strong scaling; BASELINE configs[4] when cfg5)" if args.strong
+                                else f"{args.workload}: {CONFIG_TEXT[args.workload]}"),
                    "sessions_per_gpu": S, "payload_bytes_per_session": L,
                    "global_sessions_per_step": S * ws, "rotation_batches_per_gpu": R,
+                   "job": ("fixed total split across ranks (strong)" if args.strong
+                           else "per-GPU batch replicated over ranks' own sessions (weak)"),
                    "footprint_mib_per_gpu": round(R * S * (L + 256) / 2**20, 1),
                    "parallelism": f"shard{ws} (sessions split across GPUs, no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -276,7 +293,7 @@ def kernel_name(S: int) -> str:
     except Exception:
         cus = 256
     groups = -(-S // 256)
-    return "zrc4::crypt_stream_kernel<true>" if groups > cus else "zrc4::crypt_kernel<false>"
+    return "zrc4::crypt_stream_kernel<true>" if groups > cus else "zrc4::crypt_kernel<false, true>"
 
 
 def load_traffic(workload: str):
@@ -551,6 +568,8 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--workload", choices=sorted(CONFIG_SHAPES), default="cfg2")
+    p.add_argument("--strong", action="store_true",
+                   help="the workload's sessions are the whole job, split across ranks (BASELINE configs[4])")
     p.add_argument("--footprint-mib", type=int, default=640,
                    help="rotate over distinct batches totalling this many MiB per GPU (0 = one batch)")
     p.add_argument("--cpu-seconds", type=float, default=10.0,

@@ -70,16 +70,19 @@ class OracleRunner:
         return out
 
 
-def _worker(rank, ws, port, q, workload, steps, warmup, footprint):
+def _worker(rank, ws, port, q, workload, steps, warmup, footprint, strong=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
     sys.path.insert(0, str(ROOT / "oracle"))
     import bench
     bench.CONFIG_SHAPES["tiny"] = (256, 64)
     bench.CONFIG_TEXT["tiny"] = "256 sessions x 64 B (test shape)"
+    bench.CONFIG_SHAPES["tiny2"] = (512, 64)
+    bench.CONFIG_TEXT["tiny2"] = "512 sessions x 64 B job (test shape)"
     args = bench.parse(["--workload", "cfg2", "--steps", str(steps), "--warmup", str(warmup),
                         "--footprint-mib", str(footprint), "--cpu-seconds", "0"])
     args.workload = workload
+    args.strong = strong
     res, runner = bench.run_bench(args, ws, rank, rank, backend="gloo", make_runner=OracleRunner)
     q.put((rank, res, runner.first, runner.S * runner.R,
            hashlib.sha256(runner.w.payload.tobytes()).hexdigest(), len(runner.steps_done)))
@@ -122,3 +125,31 @@ def test_two_rank_gloo_sharding_and_aggregate():
     assert [g["rank"] for g in res["per_gpu"]] == [0, 1]
     slowest = min(g["payload_gibs"] for g in res["per_gpu"])
     assert abs(slowest * ws - res["value"]) <= 0.05 * res["value"] + 2e-3
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_strong_scaling():
+    """--strong (BASELINE configs[4]): the workload's sessions are the whole
+    job; two ranks split them into disjoint halves and the aggregate counts the
+    job once."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ws, steps, warmup = 2, 2, 1
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, q, "tiny2", steps, warmup, 0, True))
+             for r in range(ws)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(ws)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    got.sort()
+    (r0, res, first0, n0, _, _), (r1, res1, first1, n1, _, _) = got
+    assert res1 is None and res is not None
+    assert n0 == n1 == 256 and (first0, first1) == (0, 256)
+    assert res["scaling"] == "strong" and res["config"]["global_sessions_per_step"] == 512
+    assert res["config"]["sessions_per_gpu"] == 256
+    total = steps * 512 * 64                                   # the job once, not per rank
+    expect = total / (res["ms_per_step"] * steps * 1e-3) / 2**30
+    assert abs(res["value"] - expect) <= 0.02 * expect + 2e-3
