@@ -380,6 +380,23 @@ def host_inclusive(args):
     per = -(-per // 256) * 256                      # whole 256-slot groups per chunk
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
     times = []
+    if args.zero_copy:
+        # the kernels read and write the pinned host buffer in place over PCIe
+        # (the session engine's pinned SessionBlock pool does the same)
+        st = streams[0]
+        for it in range(args.warmup + args.steps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ctx.crypt_range(0, host, off, ln, n=S, stream=st)
+            torch.cuda.synchronize()
+            if it >= args.warmup:
+                times.append(time.perf_counter() - t0)
+        ctx.sync(st)
+        t = statistics.median(times)
+        return {"metric": "RC4 GiB/s host-inclusive (zero-copy: kernels on pinned host memory)",
+                "value": round(S * L / t / GIB, 3), "unit": "GiB/s", "ms_per_pass": round(t * 1e3, 4),
+                "workload": args.workload, "pcie_bytes_per_pass": 2 * S * L,
+                "note": "not the headline value (DESIGN.md)"}
     for it in range(args.warmup + args.steps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -583,6 +600,8 @@ def parse(argv=None):
                    help="measure the connection-storm KSA rate instead (DESIGN.md), one JSON line")
     p.add_argument("--frame", action="store_true",
                    help="measure the device-side proto4z framing scan instead (DESIGN.md), one JSON line")
+    p.add_argument("--zero-copy", action="store_true",
+                   help="with --host-inclusive: run the kernels directly on the pinned host buffer")
     p.add_argument("--chunks", type=int, default=8)
     p.add_argument("--streams", type=int, default=3)
     return p.parse_args(argv)
