@@ -15,6 +15,9 @@
 #ifndef ZRC4_PERSIST
 #define ZRC4_PERSIST 1
 #endif
+#ifndef ZRC4_WG_PER_CU
+#define ZRC4_WG_PER_CU 2     // persistent grid size per CU (A/B knob; LDS allows 2)
+#endif
 
 struct zrc4_ctx {
     int device;
@@ -84,7 +87,7 @@ int launch_crypt(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, uint8_t 
     if (staged) {
         // persistent over groups: 2 workgroups per CU (LDS- and VGPR-limited),
         // each walking groups w, w + grid, ... (ZRC4_PERSIST=0: one group each)
-        const uint32_t wgs = ZRC4_PERSIST ? std::min(grid, 2u * (uint32_t)c->num_cus) : grid;
+        const uint32_t wgs = ZRC4_PERSIST ? std::min(grid, (uint32_t)ZRC4_WG_PER_CU * (uint32_t)c->num_cus) : grid;
         if (!ids && (first_slot & 255u) == 0u)
             hipLaunchKernelGGL(zrc4::crypt_stream_kernel<true>, dim3(wgs), dim3(zrc4::kGroup), 0, s,
                                c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,

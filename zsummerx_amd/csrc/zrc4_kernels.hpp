@@ -344,72 +344,129 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
 #define ZL_B1 "v[60:63]"
 #define ZL_B2 "v[64:67]"
 #define ZL_B3 "v[68:71]"
-#define ZL_HALF_A                                                                                \
-    "v_cmp_lt_u32_e32 vcc, %[i], %[nblk]\n\t"                                                    \
-    "s_and_b64 exec, exec, vcc\n\t"                                                              \
-    "s_cbranch_execz ZL_DONE_%=\n\t"                                                             \
+// Next block's four loads into R: from pa + 64, or -- for lanes with no next
+// block -- a harmless re-read of the current block (pa), always under the
+// loop's full exec, so every wait below counts a fixed number of VMEM ops
+// whether or not the hardware would issue an exec == 0 load.
+// pa = v[88:89], pn = v[90:91].
+#define ZL_PREFETCH(R0, R1, R2, R3)                                                              \
     "s_add_u32 %[i1], %[i], 1\n\t"                                                               \
     "v_cmp_lt_u32_e32 vcc, %[i1], %[nblk]\n\t"                                                   \
-    "s_and_saveexec_b64 %[tmp], vcc\n\t"                                                         \
-    "global_load_dwordx4 " ZL_B0 ", %[pa], off offset:64" ZRC4_LDP "\n\t"                                    \
-    "global_load_dwordx4 " ZL_B1 ", %[pa], off offset:80" ZRC4_LDP "\n\t"                                    \
-    "global_load_dwordx4 " ZL_B2 ", %[pa], off offset:96" ZRC4_LDP "\n\t"                                    \
-    "global_load_dwordx4 " ZL_B3 ", %[pa], off offset:112" ZRC4_LDP "\n\t"                                   \
-    "s_mov_b64 exec, %[tmp]\n\t"                                                                 \
+    "v_lshl_add_u64 v[90:91], v[88:89], 0, 64\n\t"                                               \
+    "v_cndmask_b32_e32 v90, v88, v90, vcc\n\t"                                                   \
+    "v_cndmask_b32_e32 v91, v89, v91, vcc\n\t"                                                   \
+    "global_load_dwordx4 " R0 ", v[90:91], off" ZRC4_LDP "\n\t"                                  \
+    "global_load_dwordx4 " R1 ", v[90:91], off offset:16" ZRC4_LDP "\n\t"                        \
+    "global_load_dwordx4 " R2 ", v[90:91], off offset:32" ZRC4_LDP "\n\t"                        \
+    "global_load_dwordx4 " R3 ", v[90:91], off offset:48" ZRC4_LDP "\n\t"
+#define ZL_STORE(R0, R1, R2, R3)                                                                 \
+    "global_store_dwordx4 v[88:89], " R0 ", off" ZRC4_STP "\n\t"                                 \
+    "global_store_dwordx4 v[88:89], " R1 ", off offset:16" ZRC4_STP "\n\t"                       \
+    "global_store_dwordx4 v[88:89], " R2 ", off offset:32" ZRC4_STP "\n\t"                       \
+    "global_store_dwordx4 v[88:89], " R3 ", off offset:48" ZRC4_STP "\n\t"                       \
+    "v_lshl_add_u64 v[88:89], v[88:89], 0, 64\n\t"                                               \
+    "s_add_u32 %[i], %[i], 1\n\t"
+#define ZL_ACTIVE                                                                                \
+    "v_cmp_lt_u32_e32 vcc, %[i], %[nblk]\n\t"                                                    \
+    "s_and_b64 exec, exec, vcc\n\t"                                                              \
+    "s_cbranch_execz ZL_DONE_%=\n\t"
+#define ZL_HALF_A                                                                                \
+    ZL_ACTIVE                                                                                    \
+    ZL_PREFETCH(ZL_B0, ZL_B1, ZL_B2, ZL_B3)                                                      \
     "s_waitcnt vmcnt(8)\n\t"                                                                     \
     ZL_BLOCK(v40, v41, v42, v43, v44, v45, v46, v47, v48, v49, v50, v51, v52, v53, v54, v55)    \
-    "global_store_dwordx4 %[pa], " ZL_A0 ", off" ZRC4_STP "\n\t"                                             \
-    "global_store_dwordx4 %[pa], " ZL_A1 ", off offset:16" ZRC4_STP "\n\t"                                   \
-    "global_store_dwordx4 %[pa], " ZL_A2 ", off offset:32" ZRC4_STP "\n\t"                                   \
-    "global_store_dwordx4 %[pa], " ZL_A3 ", off offset:48" ZRC4_STP "\n\t"                                   \
-    "v_lshl_add_u64 %[pa], %[pa], 0, 64\n\t"                                                     \
-    "s_add_u32 %[i], %[i], 1\n\t"
+    ZL_STORE(ZL_A0, ZL_A1, ZL_A2, ZL_A3)
 #define ZL_HALF_B                                                                                \
-    "v_cmp_lt_u32_e32 vcc, %[i], %[nblk]\n\t"                                                    \
-    "s_and_b64 exec, exec, vcc\n\t"                                                              \
-    "s_cbranch_execz ZL_DONE_%=\n\t"                                                             \
-    "s_add_u32 %[i1], %[i], 1\n\t"                                                               \
-    "v_cmp_lt_u32_e32 vcc, %[i1], %[nblk]\n\t"                                                   \
-    "s_and_saveexec_b64 %[tmp], vcc\n\t"                                                         \
-    "global_load_dwordx4 " ZL_A0 ", %[pa], off offset:64" ZRC4_LDP "\n\t"                                    \
-    "global_load_dwordx4 " ZL_A1 ", %[pa], off offset:80" ZRC4_LDP "\n\t"                                    \
-    "global_load_dwordx4 " ZL_A2 ", %[pa], off offset:96" ZRC4_LDP "\n\t"                                    \
-    "global_load_dwordx4 " ZL_A3 ", %[pa], off offset:112" ZRC4_LDP "\n\t"                                   \
-    "s_mov_b64 exec, %[tmp]\n\t"                                                                 \
+    ZL_ACTIVE                                                                                    \
+    ZL_PREFETCH(ZL_A0, ZL_A1, ZL_A2, ZL_A3)                                                      \
     "s_waitcnt vmcnt(8)\n\t"                                                                     \
     ZL_BLOCK(v56, v57, v58, v59, v60, v61, v62, v63, v64, v65, v66, v67, v68, v69, v70, v71)    \
-    "global_store_dwordx4 %[pa], " ZL_B0 ", off" ZRC4_STP "\n\t"                                             \
-    "global_store_dwordx4 %[pa], " ZL_B1 ", off offset:16" ZRC4_STP "\n\t"                                   \
-    "global_store_dwordx4 %[pa], " ZL_B2 ", off offset:32" ZRC4_STP "\n\t"                                   \
-    "global_store_dwordx4 %[pa], " ZL_B3 ", off offset:48" ZRC4_STP "\n\t"                                   \
-    "v_lshl_add_u64 %[pa], %[pa], 0, 64\n\t"                                                     \
-    "s_add_u32 %[i], %[i], 1\n\t"
+    ZL_STORE(ZL_B0, ZL_B1, ZL_B2, ZL_B3)
+
+// Block 0 with its keystream generated AHEAD of its payload (ZRC4_LEAD=1):
+// the 64 keystream bytes go into K = v72..v87 (cleared), and only then does
+// the wave wait for block 0's loads -- vmcnt(4): block 1's four prefetch
+// loads are the only younger VMEM ops -- and XOR K into A.  When the caller
+// issued block 0 from asm right before the LDS fill (issue_block_asm), its
+// HBM round trip overlaps 64 PRGA steps instead of stalling the wave at the
+// top of the loop (hipcc drained it with a vmcnt(0) there).
+#define ZL_FIRST                                                                                 \
+    "s_mov_b32 %[i], 0\n\t"                                                                      \
+    ZL_PREFETCH(ZL_B0, ZL_B1, ZL_B2, ZL_B3)                                                      \
+    "v_mov_b32 v72, 0\n\tv_mov_b32 v73, 0\n\tv_mov_b32 v74, 0\n\tv_mov_b32 v75, 0\n\t"             \
+    "v_mov_b32 v76, 0\n\tv_mov_b32 v77, 0\n\tv_mov_b32 v78, 0\n\tv_mov_b32 v79, 0\n\t"             \
+    "v_mov_b32 v80, 0\n\tv_mov_b32 v81, 0\n\tv_mov_b32 v82, 0\n\tv_mov_b32 v83, 0\n\t"             \
+    "v_mov_b32 v84, 0\n\tv_mov_b32 v85, 0\n\tv_mov_b32 v86, 0\n\tv_mov_b32 v87, 0\n\t"             \
+    ZL_BLOCK(v72, v73, v74, v75, v76, v77, v78, v79, v80, v81, v82, v83, v84, v85, v86, v87)    \
+    "s_waitcnt vmcnt(4)\n\t"                                                                     \
+    "v_xor_b32_e32 v40, v40, v72\n\tv_xor_b32_e32 v41, v41, v73\n\t"                               \
+    "v_xor_b32_e32 v42, v42, v74\n\tv_xor_b32_e32 v43, v43, v75\n\t"                               \
+    "v_xor_b32_e32 v44, v44, v76\n\tv_xor_b32_e32 v45, v45, v77\n\t"                               \
+    "v_xor_b32_e32 v46, v46, v78\n\tv_xor_b32_e32 v47, v47, v79\n\t"                               \
+    "v_xor_b32_e32 v48, v48, v80\n\tv_xor_b32_e32 v49, v49, v81\n\t"                               \
+    "v_xor_b32_e32 v50, v50, v82\n\tv_xor_b32_e32 v51, v51, v83\n\t"                               \
+    "v_xor_b32_e32 v52, v52, v84\n\tv_xor_b32_e32 v53, v53, v85\n\t"                               \
+    "v_xor_b32_e32 v54, v54, v86\n\tv_xor_b32_e32 v55, v55, v87\n\t"                               \
+    ZL_STORE(ZL_A0, ZL_A1, ZL_A2, ZL_A3)                                                         \
+    "s_branch ZL_MID_%=\n\t"
+#ifndef ZRC4_LEAD
+#define ZRC4_LEAD 1
+#endif
 
 __device__ __forceinline__ void crypt_blocks_asm(Rc4Lane &st, uint4 *&p, uint32_t nblk,
                                                  const uint4 (&A)[4])
 {
     u32x4 a0 = {A[0].x, A[0].y, A[0].z, A[0].w}, a1 = {A[1].x, A[1].y, A[1].z, A[1].w};
     u32x4 a2 = {A[2].x, A[2].y, A[2].z, A[2].w}, a3 = {A[3].x, A[3].y, A[3].z, A[3].w};
-    u32x4 b0, b1, b2, b3;
-    uint64_t pa = (uint64_t)(uintptr_t)p, save, tmp;
+    u32x4 b0, b1, b2, b3, q0, q1, q2, q3;
+    uint64_t pa = (uint64_t)(uintptr_t)p, pn, save;
     uint32_t i, i1, b, k0, k1, a1s;
     asm volatile(
         "s_mov_b64 %[save], exec\n\t"
+#if ZRC4_LEAD
+        ZL_FIRST
+#else
         "s_mov_b32 %[i], 0\n\t"
+#endif
         "ZL_LOOP_%=:\n\t"
         ZL_HALF_A
+        "ZL_MID_%=:\n\t"
         ZL_HALF_B
         "s_branch ZL_LOOP_%=\n\t"
         "ZL_DONE_%=:\n\t"
         "s_mov_b64 exec, %[save]\n\t"
         : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1),
           [a0] "+v"(st.a0), [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
-          [pa] "+v"(pa), [i] "=&s"(i), [i1] "=&s"(i1), [save] "=&s"(save), [tmp] "=&s"(tmp),
+          "+{v[88:89]}"(pa), "=&{v[90:91]}"(pn), [i] "=&s"(i), [i1] "=&s"(i1), [save] "=&s"(save),
           "+{v[40:43]}"(a0), "+{v[44:47]}"(a1), "+{v[48:51]}"(a2), "+{v[52:55]}"(a3),
-          "=&{v[56:59]}"(b0), "=&{v[60:63]}"(b1), "=&{v[64:67]}"(b2), "=&{v[68:71]}"(b3)
+          "=&{v[56:59]}"(b0), "=&{v[60:63]}"(b1), "=&{v[64:67]}"(b2), "=&{v[68:71]}"(b3),
+          "=&{v[72:75]}"(q0), "=&{v[76:79]}"(q1), "=&{v[80:83]}"(q2), "=&{v[84:87]}"(q3)
         : [nblk] "v"(nblk)
         : "memory", "vcc", "scc");
     p = reinterpret_cast<uint4 *>((uintptr_t)pa);
+}
+
+// Block 0 of a message issued from asm into the pinned A tuples, so hipcc
+// neither counts nor waits for it (crypt_blocks_asm's lead block does).
+__device__ __forceinline__ void issue_block_asm(uint4 (&A)[4], const uint8_t *msg)
+{
+#if ZRC4_LEAD
+    u32x4 a0, a1, a2, a3;
+    asm volatile(
+        "global_load_dwordx4 v[40:43], %[p], off" ZRC4_LDP "\n\t"
+        "global_load_dwordx4 v[44:47], %[p], off offset:16" ZRC4_LDP "\n\t"
+        "global_load_dwordx4 v[48:51], %[p], off offset:32" ZRC4_LDP "\n\t"
+        "global_load_dwordx4 v[52:55], %[p], off offset:48" ZRC4_LDP "\n\t"
+        : "=&{v[40:43]}"(a0), "=&{v[44:47]}"(a1), "=&{v[48:51]}"(a2), "=&{v[52:55]}"(a3)
+        : [p] "v"(msg)
+        : "memory");
+    A[0] = make_uint4(a0[0], a0[1], a0[2], a0[3]);
+    A[1] = make_uint4(a1[0], a1[1], a1[2], a1[3]);
+    A[2] = make_uint4(a2[0], a2[1], a2[2], a2[3]);
+    A[3] = make_uint4(a3[0], a3[1], a3[2], a3[3]);
+#else
+    load64(A, reinterpret_cast<const uint4 *>(msg));
+#endif
 }
 
 #ifndef ZRC4_ASM_LOOP
@@ -431,7 +488,7 @@ __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st, uint8_t *
     uint4 *p = reinterpret_cast<uint4 *>(msg);
     const uint32_t nblk = len >> 6;
     if (ZRC4_ASM_LOOP && nblk) {
-        if (!pre) load64(A, p);
+        if (!pre) issue_block_asm(A, reinterpret_cast<const uint8_t *>(p));
         crypt_blocks_asm(st, p, nblk, A);
     } else if (nblk) {
         // Ping-pong buffers A/B, no loop-carried copies, and the next block's
@@ -1063,16 +1120,16 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #pragma unroll
             for (int i = 0; i < 16; ++i) img[i] = src[i * 256 + j];
         }
-        if (pre) load64(A, reinterpret_cast<const uint4 *>(msg));
+        if (pre) issue_block_asm(A, msg);
         uint4 *dst = reinterpret_cast<uint4 *>(S);
 #pragma unroll
         for (int i = 0; i < 16; ++i) dst[i * 256 + j] = img[i];
         } else if (pre) {
-            load64(A, reinterpret_cast<const uint4 *>(msg));
+            issue_block_asm(A, msg);
         }
         __syncthreads();
     } else {
-        if (pre) load64(A, reinterpret_cast<const uint4 *>(msg));
+        if (pre) issue_block_asm(A, msg);
         if (active && mylen) gather_column(S, col, arena, slot);
     }
 
