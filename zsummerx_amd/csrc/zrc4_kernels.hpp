@@ -290,6 +290,9 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
 #ifndef ZRC4_IMG_NT
 #define ZRC4_IMG_NT 0
 #endif
+#ifndef ZRC4_DIRECT_IMG_NT
+#define ZRC4_DIRECT_IMG_NT 0   // crypt_kernel's epilogue image store with nt (A/B knob)
+#endif
 #ifndef ZRC4_LL_STP_MODE
 #define ZRC4_LL_STP_MODE 2
 #endif
@@ -1168,7 +1171,12 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 
     if (whole) {
         __syncthreads();
-        if (!(ZRC4_ABLATE & 16)) lds_to_image(arena + (size_t)g * kGroupBytes, S);
+        if (ZRC4_ABLATE & 16) {
+        } else if (ZRC4_DIRECT_IMG_NT) {
+            lds_to_image_nt(arena + (size_t)g * kGroupBytes, S);
+        } else {
+            lds_to_image(arena + (size_t)g * kGroupBytes, S);
+        }
     } else if (active && mylen) {
         scatter_column(arena, slot, S, col);
     }
