@@ -256,6 +256,51 @@ def test_staged_path_ragged(built, torch_cuda, ids_kind):
             assert (sb, x, y) == (bytes(want_sb), wx, wy), i
 
 
+# ------------------------------- direct (chain-bound) path, block-loop edges
+@pytest.mark.parametrize("first_slot", [0, 256])
+def test_direct_path_block_edges(built, torch_cuda, first_slot):
+    """One workgroup per CU selects crypt_kernel's direct block loop (lead
+    block, static-count prefetch).  Group 0: every lane exactly one 64-byte
+    block (the first block's prefetch re-reads it for every lane of every
+    wave); group 1: exactly two; group 2: lengths cycling through the block
+    edges with zeros mixed in; group 3: 16-byte aligned messages that start
+    mid-line.  Gaps between messages must stay untouched; three calls in a
+    row continue the keystream (state write-back)."""
+    torch = torch_cuda
+    n = 4 * 256
+    rng = np.random.default_rng(21 + first_slot)
+    keys = rng.integers(0, 256, 16 * n, dtype=np.uint8)
+    koff = np.arange(n, dtype=np.uint64) * 16
+    klen = np.full(n, 16, dtype=np.uint32)
+    ob = pyoracle.Batch(n)
+    ob.make_sbox(keys, koff, klen)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    edges = [0, 1, 15, 16, 17, 63, 64, 65, 127, 128, 129, 191, 192, 193, 255, 256, 320, 1000, 1024, 0]
+    s = torch.cuda.current_stream()
+    with Context(0, first_slot + n) as c:
+        c.ksa_range(first_slot, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
+        for call in range(3):
+            L = np.concatenate([np.full(256, 64), np.full(256, 128),
+                                np.resize(edges, 256), rng.integers(0, 400, 256)]).astype(np.uint32)
+            rng.shuffle(L[512:768])
+            stride = 1536
+            off = np.arange(n, dtype=np.uint64) * stride
+            off[768:] += (rng.integers(0, 8, 256) * 16).astype(np.uint64)   # aligned, mid-line
+            data = rng.integers(0, 256, n * stride + 256, dtype=np.uint8)
+            want = data.copy()
+            ob.crypt(want, off, L, threads=8)
+            pay = T(data)
+            c.crypt_range(first_slot, pay, T(off.view(np.int64)), T(L.view(np.int32)), stream=s)
+            c.sync(s)
+            got = pay.cpu().numpy()
+            bad = np.flatnonzero(got != want)
+            assert bad.size == 0, (call, bad[:8], int(bad.size))
+        for i in (0, 255, 256, 511, 600, 767, 800, n - 1):
+            sb, x, y = c.get_state(first_slot + i)
+            want_sb, wx, wy = ob.state(i)
+            assert (sb, x, y) == (bytes(want_sb), wx, wy), i
+
+
 # ------------------------------------------------ full BASELINE-size configs
 def _device_workload(ctx, w, torch):
     dev = "cuda"
