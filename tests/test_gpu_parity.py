@@ -69,6 +69,35 @@ def test_edge_cases(ctx, edge):
         assert state_of(ctx, slot) == (c["state"]["sbox"], c["state"]["x"], c["state"]["y"]), c["name"]
 
 
+def test_ksa_key_lengths_batched(built, torch_cuda):
+    """Batched makeSBox over key lengths 0..40, 64, 255, 256, 257, 300 (the
+    register-pattern path takes lengths 1, 2, 4, 8, 16; every other length
+    fetches key bytes per step), NUL bytes included, keys at odd offsets;
+    whole groups (range) and scattered ids; states against the oracle."""
+    torch = torch_cuda
+    rng = np.random.default_rng(31)
+    lens = list(range(0, 41)) + [64, 255, 256, 257, 300]
+    n = 512
+    klen = np.array([lens[i % len(lens)] for i in range(n)], dtype=np.uint32)
+    koff = (np.concatenate([[3], np.cumsum(klen[:-1] + 1) + 3])).astype(np.uint64)
+    keys = rng.integers(0, 256, int(koff[-1] + klen[-1]) + 8, dtype=np.uint8)
+    keys[::7] = 0
+    ob = pyoracle.Batch(n)
+    ob.make_sbox(keys, koff, klen)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    s = torch.cuda.current_stream()
+    for ids in (None, rng.permutation(2 * n)[:n].astype(np.uint32)):
+        with Context(0, 2 * n) as c:
+            c.ksa(T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys),
+                  ids=None if ids is None else T(ids.view(np.int32)), stream=s)
+            c.sync(s)
+            for i in range(n):
+                slot = i if ids is None else int(ids[i])
+                sb, x, y = c.get_state(slot)
+                want_sb, wx, wy = ob.state(i)
+                assert (sb, x, y) == (bytes(want_sb), wx, wy), (i, int(klen[i]))
+
+
 def test_rc4encryption_mirror_class(built, kat):
     v = kat["wikipedia"][2]
     r = RC4Encryption()
