@@ -1441,21 +1441,26 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 // swaps the reference's order (:63-64); they only collide when i == j, and
 // then b == a.  Key bytes for 16 steps are fetched one chunk ahead.
 // ---------------------------------------------------------------------------
-#define ZRC4_KSA_STEP(XC, XN, A, P, KN)                                                          \
+#define ZRC4_KSA_STEP_SEL(XC, XN, A, P, KN, SEL)                                                 \
     "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
     "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
     "ds_read_u8 %[b], %[ya]\n\t"                                                                 \
     "ds_write_b8 %[ya], %[" #A "]\n\t"                                                           \
     "ds_read_u8 %[" #P "], %[" #XN "]\n\t"                                                       \
     "v_add_u32_sdwa %[ya], %[ya], %[" #KN "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "         \
-    "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
+    "src0_sel:BYTE_1 src1_sel:" #SEL "\n\t"                                                      \
     "s_waitcnt lgkmcnt(2)\n\t"                                                                   \
     "ds_write_b8 %[" #XC "], %[b]\n\t"                                                           \
     "v_add_u32_sdwa %[" #XC "], 1, %[" #XN "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "        \
     "src0_sel:DWORD src1_sel:BYTE_1\n\t"                                                         \
     "s_waitcnt lgkmcnt(1)\n\t"
+#define ZRC4_KSA_STEP(XC, XN, A, P, KN) ZRC4_KSA_STEP_SEL(XC, XN, A, P, KN, BYTE_0)
 #define ZRC4_KSA_PAIR(K1, K2)                                                                    \
     ZRC4_KSA_STEP(x0, x1, a0, a1, K1) ZRC4_KSA_STEP(x1, x0, a1, a0, K2)
+// Key pattern in 4 registers (byte u of q = key[u % len], len | 16): step u
+// of a 16-step chunk adds pattern byte (u + 1) % 16.
+#define ZRC4_KSA_QPAIR(K1, S1, K2, S2)                                                           \
+    ZRC4_KSA_STEP_SEL(x0, x1, a0, a1, K1, S1) ZRC4_KSA_STEP_SEL(x1, x0, a1, a0, K2, S2)
 
 // 16 KSA steps.  In: x0 = &S[i], x1 = &S[i+1], a0 = S[i], ya = &S[j + key[i]].
 // kn[u] = key byte of step i+u+1 (kn[15] = first byte of the next chunk).
@@ -1475,8 +1480,29 @@ __device__ __forceinline__ void ksa16_asm(uint32_t &x0, uint32_t &x1, uint32_t &
         : "memory");
 }
 
+// 16 KSA steps with the key bytes taken from a 16-byte pattern in registers
+// (key lengths 1, 2, 4, 8, 16: key[k mod len] repeats every 16 steps), so the
+// loop issues no key loads at all.
+__device__ __forceinline__ void ksa16_pattern_asm(uint32_t &x0, uint32_t &x1, uint32_t &a0, uint32_t &ya,
+                                                  const uint32_t (&q)[4])
+{
+    uint32_t a1, b;
+    asm volatile(
+        ZRC4_KSA_QPAIR(q0, BYTE_1, q0, BYTE_2) ZRC4_KSA_QPAIR(q0, BYTE_3, q1, BYTE_0)
+        ZRC4_KSA_QPAIR(q1, BYTE_1, q1, BYTE_2) ZRC4_KSA_QPAIR(q1, BYTE_3, q2, BYTE_0)
+        ZRC4_KSA_QPAIR(q2, BYTE_1, q2, BYTE_2) ZRC4_KSA_QPAIR(q2, BYTE_3, q3, BYTE_0)
+        ZRC4_KSA_QPAIR(q3, BYTE_1, q3, BYTE_2) ZRC4_KSA_QPAIR(q3, BYTE_3, q0, BYTE_0)
+        "s_waitcnt lgkmcnt(0)\n\t"
+        : [ya] "+v"(ya), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0), [a1] "=&v"(a1), [b] "=&v"(b)
+        : [q0] "v"(q[0]), [q1] "v"(q[1]), [q2] "v"(q[2]), [q3] "v"(q[3])
+        : "memory");
+}
+
 #ifndef ZRC4_KSA_ASM
 #define ZRC4_KSA_ASM 1      // 0: the portable C step (A/B builds)
+#endif
+#ifndef ZRC4_KSA_PATTERN
+#define ZRC4_KSA_PATTERN 1  // key lengths dividing 16 keep the key schedule in registers (0: A/B builds)
 #endif
 
 __global__ void __launch_bounds__(256, 2)
@@ -1537,7 +1563,16 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     }
 
     if (active && kl) {
-        if (ZRC4_KSA_ASM) {
+        constexpr bool kPattern = (ZRC4_KSA_ASM != 0) && (ZRC4_KSA_PATTERN != 0);
+        if (kPattern && kl <= 16u && (16u % kl) == 0u) {
+            // the whole key schedule (:67-70) in 16 register bytes, loaded once
+            uint32_t q[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int u = 0; u < 16; ++u) q[u >> 2] |= (uint32_t)key[(uint32_t)u & (kl - 1u)] << (8 * (u & 3));
+            uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col];
+            uint32_t ya = col | ((q[0] & 0xFFu) << 8);    // j = 0 + key[0] before step 0
+            for (int c = 0; c < 16; ++c) ksa16_pattern_asm(x0, x1, a0, ya, q);
+        } else if (ZRC4_KSA_ASM) {
             // key bytes of steps 16c .. 16c+16, fetched one chunk ahead
             uint32_t kk = 0;
             auto fetch = [&](uint32_t (&kb)[17]) {
