@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--footprint-mib", type=int, default=640)
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--ksa", action="store_true", help="also time zrc4_ksa_range per variant")
+    ap.add_argument("--key-len", type=int, default=16, help="key bytes per session (16: the synthetic keys)")
     ap.add_argument("--segment", action="store_true",
                     help="time each round's launches as one back-to-back segment (per-launch average)")
     ap.add_argument("--no-check", action="store_true", help="timing-only ablation builds (outputs differ)")
@@ -79,10 +80,14 @@ def main():
         R = max(1, -(-args.footprint_mib * (1 << 20) // (S * (L + 256))))
         R = min(R, (1 << 24) // S)
         n = S * R
-        keys = torch.from_numpy(synth.keys(0, n).reshape(-1)).to(dev)
+        KL = args.key_len
+        if KL == 16:
+            keys = torch.from_numpy(synth.keys(0, n).reshape(-1)).to(dev)
+        else:
+            keys = torch.from_numpy(np.random.default_rng(1).integers(0, 256, n * KL, dtype=np.uint8)).to(dev)
         adv = torch.from_numpy(synth.advance(0, n).view(np.int32)).to(dev)
-        klen = torch.full((n,), 16, dtype=torch.int32, device=dev)
-        koff = torch.arange(n, dtype=torch.int64, device=dev) * 16
+        klen = torch.full((n,), KL, dtype=torch.int32, device=dev)
+        koff = torch.arange(n, dtype=torch.int64, device=dev) * KL
         pay = torch.from_numpy(synth.payload(0, n * L, threads=8)).to(dev)
         off = torch.arange(n, dtype=torch.int64, device=dev) * L
         ln = torch.full((n,), L, dtype=torch.int32, device=dev)

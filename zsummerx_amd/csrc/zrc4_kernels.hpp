@@ -1457,8 +1457,8 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #define ZRC4_KSA_STEP(XC, XN, A, P, KN) ZRC4_KSA_STEP_SEL(XC, XN, A, P, KN, BYTE_0)
 #define ZRC4_KSA_PAIR(K1, K2)                                                                    \
     ZRC4_KSA_STEP(x0, x1, a0, a1, K1) ZRC4_KSA_STEP(x1, x0, a1, a0, K2)
-// Key pattern in 4 registers (byte u of q = key[u % len], len | 16): step u
-// of a 16-step chunk adds pattern byte (u + 1) % 16.
+// Key pattern in registers (byte u of q = key[u % len]): step u of a 16- or
+// 64-step chunk adds pattern byte (u + 1) mod the chunk length.
 #define ZRC4_KSA_QPAIR(K1, S1, K2, S2)                                                           \
     ZRC4_KSA_STEP_SEL(x0, x1, a0, a1, K1, S1) ZRC4_KSA_STEP_SEL(x1, x0, a1, a0, K2, S2)
 
@@ -1481,8 +1481,7 @@ __device__ __forceinline__ void ksa16_asm(uint32_t &x0, uint32_t &x1, uint32_t &
 }
 
 // 16 KSA steps with the key bytes taken from a 16-byte pattern in registers
-// (key lengths 1, 2, 4, 8, 16: key[k mod len] repeats every 16 steps), so the
-// loop issues no key loads at all.
+// (key lengths 1, 2, 4, 8, 16).  Step u adds pattern byte (u+1) % 16.
 __device__ __forceinline__ void ksa16_pattern_asm(uint32_t &x0, uint32_t &x1, uint32_t &a0, uint32_t &ya,
                                                   const uint32_t (&q)[4])
 {
@@ -1498,11 +1497,33 @@ __device__ __forceinline__ void ksa16_pattern_asm(uint32_t &x0, uint32_t &x1, ui
         : "memory");
 }
 
+// 64 KSA steps with the key bytes taken from a 64-byte pattern in registers
+// (key lengths 32 and 64: key[k mod len] repeats every 64 steps), so the loop
+// issues no key loads at all.  Step u adds pattern byte (u+1) % 64.
+#define ZRC4_KSA_Q4(QA, QB) ZRC4_KSA_QPAIR(QA, BYTE_1, QA, BYTE_2) ZRC4_KSA_QPAIR(QA, BYTE_3, QB, BYTE_0)
+__device__ __forceinline__ void ksa64_pattern_asm(uint32_t &x0, uint32_t &x1, uint32_t &a0, uint32_t &ya,
+                                                  const uint32_t (&q)[16])
+{
+    uint32_t a1, b;
+    asm volatile(
+        ZRC4_KSA_Q4(q0, q1) ZRC4_KSA_Q4(q1, q2) ZRC4_KSA_Q4(q2, q3) ZRC4_KSA_Q4(q3, q4)
+        ZRC4_KSA_Q4(q4, q5) ZRC4_KSA_Q4(q5, q6) ZRC4_KSA_Q4(q6, q7) ZRC4_KSA_Q4(q7, q8)
+        ZRC4_KSA_Q4(q8, q9) ZRC4_KSA_Q4(q9, q10) ZRC4_KSA_Q4(q10, q11) ZRC4_KSA_Q4(q11, q12)
+        ZRC4_KSA_Q4(q12, q13) ZRC4_KSA_Q4(q13, q14) ZRC4_KSA_Q4(q14, q15) ZRC4_KSA_Q4(q15, q0)
+        "s_waitcnt lgkmcnt(0)\n\t"
+        : [ya] "+v"(ya), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0), [a1] "=&v"(a1), [b] "=&v"(b)
+        : [q0] "v"(q[0]), [q1] "v"(q[1]), [q2] "v"(q[2]), [q3] "v"(q[3]), [q4] "v"(q[4]),
+          [q5] "v"(q[5]), [q6] "v"(q[6]), [q7] "v"(q[7]), [q8] "v"(q[8]), [q9] "v"(q[9]),
+          [q10] "v"(q[10]), [q11] "v"(q[11]), [q12] "v"(q[12]), [q13] "v"(q[13]),
+          [q14] "v"(q[14]), [q15] "v"(q[15])
+        : "memory");
+}
+
 #ifndef ZRC4_KSA_ASM
 #define ZRC4_KSA_ASM 1      // 0: the portable C step (A/B builds)
 #endif
 #ifndef ZRC4_KSA_PATTERN
-#define ZRC4_KSA_PATTERN 1  // key lengths dividing 16 keep the key schedule in registers (0: A/B builds)
+#define ZRC4_KSA_PATTERN 1  // key lengths 1-16 (dividing 16), 32 and 64 keep the key schedule in registers (0: A/B builds)
 #endif
 
 __global__ void __launch_bounds__(256, 2)
@@ -1572,6 +1593,16 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col];
             uint32_t ya = col | ((q[0] & 0xFFu) << 8);    // j = 0 + key[0] before step 0
             for (int c = 0; c < 16; ++c) ksa16_pattern_asm(x0, x1, a0, ya, q);
+        } else if (kPattern && (kl == 32u || kl == 64u)) {
+            // 32- and 64-byte keys: the schedule in 64 register bytes
+            uint32_t q[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) q[i] = 0u;
+#pragma unroll
+            for (int u = 0; u < 64; ++u) q[u >> 2] |= (uint32_t)key[(uint32_t)u & (kl - 1u)] << (8 * (u & 3));
+            uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col];
+            uint32_t ya = col | ((q[0] & 0xFFu) << 8);
+            for (int c = 0; c < 4; ++c) ksa64_pattern_asm(x0, x1, a0, ya, q);
         } else if (ZRC4_KSA_ASM) {
             // key bytes of steps 16c .. 16c+16, fetched one chunk ahead
             uint32_t kk = 0;
