@@ -37,7 +37,11 @@
  *   - device-side faults of a batched call (a slot id >= capacity) are latched
  *     and reported by the next zrc4_sync() as ZRC4_ERR_SLOT_RANGE; the affected
  *     entries are skipped (caller closes those sessions, as the reference does
- *     on BCT_CORRUPTION, src/frame/session.cpp:355-361).
+ *     on BCT_CORRUPTION, src/frame/session.cpp:355-361).  The latch belongs to
+ *     the CONTEXT, not to a stream: zrc4_sync on any stream reports (and
+ *     clears) faults of every kernel of the context that has completed, so a
+ *     caller that uses several streams syncs them all before acting on a
+ *     fault.
  */
 #ifndef ZRC4_H
 #define ZRC4_H
@@ -56,6 +60,8 @@ extern "C" {
 #define ZRC4_ERR_LAUNCH (-4)
 #define ZRC4_ERR_SLOT_RANGE (-5)
 #define ZRC4_ERR_HIP (-6)
+#define ZRC4_ERR_GROUP (-7)    /* zrc4_crypt_grouped: a bucket mixes slot groups */
+#define ZRC4_ERR_INTERNAL (-8) /* kernel self-check failed (LDS layout) */
 
 /* Slots are grouped 256 to a 64 KiB device image (the LDS image of one
  * workgroup); capacity is rounded up to a multiple of this. */
@@ -96,6 +102,21 @@ int zrc4_ksa_range(zrc4_ctx *ctx, uint32_t first_slot, const uint8_t *keys,
 int zrc4_crypt_range(zrc4_ctx *ctx, uint32_t first_slot, uint8_t *payload,
                      const uint64_t *off, const uint32_t *len, uint32_t n,
                      void *stream);
+
+/* Grouped-ids variant: the fast path for arbitrary slot subsets.  Entries
+ * are taken in buckets of 256 (bucket b = entries [256b, 256b + 256)); the
+ * caller promises that every busy entry (len > 0) of a bucket uses a slot of
+ * ONE 256-slot group (slot / 256), that no other bucket of the call touches
+ * that group, and that a slot appears at most once.  Entries may come in any
+ * order; padding entries carry ids[i] = ZRC4_IDLE_SLOT or len 0.  Each bucket
+ * then moves its group's state as one coalesced 64 KiB image, exactly like a
+ * whole-group zrc4_crypt_range.  A bucket whose busy entries span two groups
+ * is skipped and reported by zrc4_sync as ZRC4_ERR_GROUP.  Device pointers;
+ * asynchronous. */
+#define ZRC4_IDLE_SLOT 0xFFFFFFFFu
+int zrc4_crypt_grouped(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payload,
+                       const uint64_t *off, const uint32_t *len, uint32_t n,
+                       void *stream);
 
 /* Host-pointer variants: copy to the device (pinned staging), run, copy back,
  * block until done.  payload_bytes bounds the host payload buffer. */

@@ -71,6 +71,13 @@ class Server:
             self.p.kill()
             raise RuntimeError(f"server did not start: {line!r} {self.p.stderr.read()}")
         self.port = int(line.split()[1])
+        self.port2 = None
+        if "--plain-accepter" in extra:
+            line = self.p.stdout.readline()
+            if not line.startswith("PORT2 "):
+                self.p.kill()
+                raise RuntimeError(f"server did not open the plain accepter: {line!r}")
+            self.port2 = int(line.split()[1])
 
     def finish(self, timeout=60):
         out, err = self.p.communicate(timeout=timeout)
@@ -78,12 +85,20 @@ class Server:
         return json.loads(out.strip().splitlines()[-1])
 
 
-def echo_client(port, seed, npk, results, idx):
-    """Send npk proto4z packets, RC4-encrypted with the oracle, in random
-    chunkings (splits inside headers and bodies, several packets per write);
-    read the echoes back and decrypt them with the oracle."""
+class _Plain:
+    """RC4 off (_rc4TcpEncryption empty): the wire carries the plaintext."""
+
+    def encryption(self, b):
+        return bytes(b)
+
+
+def echo_client(port, seed, npk, results, idx, keyed=True):
+    """Send npk proto4z packets, RC4-encrypted with the oracle (or in clear
+    when keyed is False), in random chunkings (splits inside headers and
+    bodies, several packets per write); read the echoes back and decrypt them
+    with the oracle."""
     rng = random.Random(seed)
-    wr, rd = rc4(), rc4()                      # session.cpp:110-111: same key both ways
+    wr, rd = (rc4(), rc4()) if keyed else (_Plain(), _Plain())   # session.cpp:110-111: same key both ways
     plain = b"".join(packet(rng, rng.choice([8, 9, 64, 1000, 1024, 4096, 20000, rng.randint(8, 3000)]), i)
                      for i in range(npk))
     wire = wr.encryption(plain)
@@ -132,6 +147,38 @@ def run_echo_parity(stress, hooks, nclients=6, npk=40):
         assert decrypted == plain
     assert stats["recv_packs"] == nclients * npk
     assert stats["linked"] == nclients
+    return stats
+
+
+def run_mixed_keyed_plain(stress, hooks, nclients=4, npk=30):
+    """Row a6 (config.h:196, session.cpp:313-316): ONE engine, ONE hooks
+    object, keyed and keyless sessions in the same event-loop iterations.
+    Keyed sessions must echo reference RC4 on the wire, keyless ones the
+    plaintext itself, and neither may disturb the other's keystream."""
+    srv = Server(stress, hooks, 2 * nclients, "--plain-accepter")
+    results = [None] * (2 * nclients)
+    th = [threading.Thread(target=echo_client, args=(srv.port if i % 2 == 0 else srv.port2, 2000 + i, npk,
+                                                      results, i, i % 2 == 0))
+          for i in range(2 * nclients)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    if any(r is None for r in results):
+        srv.p.kill()
+        _, err = srv.p.communicate(timeout=30)
+        raise AssertionError(f"clients {[i for i, r in enumerate(results) if r is None]} did not finish; "
+                             f"server stderr: {err[-3000:]}")
+    stats = srv.finish()
+    for i, (plain, wire, decrypted) in enumerate(results):
+        if i % 2 == 0:
+            assert wire == rc4().encryption(plain), f"keyed client {i}: wire is not the reference RC4"
+            assert wire != plain
+        else:
+            assert wire == plain, f"keyless client {i}: wire must be the plaintext (RC4 off)"
+        assert decrypted == plain
+    assert stats["recv_packs"] == 2 * nclients * npk
+    assert stats["linked"] == 2 * nclients
     return stats
 
 
@@ -240,6 +287,15 @@ def test_engine_echo_parity_cpu_hooks(stress):
     run_echo_parity(stress, ORACLE_HOOKS)
 
 
+def test_mixed_keyed_and_keyless_emulated_device_hooks(stress_emu):
+    st = run_mixed_keyed_plain(stress_emu, "device")
+    assert st["rc4"] == "zrc4-gfx950"
+
+
+def test_mixed_keyed_and_keyless_cpu_hooks(stress):
+    run_mixed_keyed_plain(stress, ORACLE_HOOKS)
+
+
 def test_engine_as_client_cpu_hooks(stress):
     run_engine_client(stress, ORACLE_HOOKS)
 
@@ -275,6 +331,18 @@ def test_no_device_is_loud(stress):
 def test_engine_echo_parity_device(stress):
     st = run_echo_parity(stress, "device")
     assert st["rc4"] == "zrc4-gfx950"
+
+
+@pytest.mark.gpu
+def test_mixed_keyed_and_keyless_device(stress):
+    st = run_mixed_keyed_plain(stress, "device")
+    assert st["rc4"] == "zrc4-gfx950"
+
+
+@pytest.mark.gpu
+def test_mixed_keyed_and_keyless_device_direct(stress):
+    st = run_mixed_keyed_plain(stress, "device-direct")
+    assert st["rc4"] == "zrc4-gfx950-direct"
 
 
 @pytest.mark.gpu

@@ -110,6 +110,7 @@ struct Args {
     unsigned exitAfter = 0;       // server: exit after this many sessions closed
     unsigned echoes = 0;          // client: close a session after this many echoes (0 = run by time)
     bool flashPolicy = false;
+    bool plainAccepter = false;   // server: a second accepter with RC4 off (empty key, config.h:196)
     int device = 0;
     unsigned ring = 32768;        // keystream reservoir bytes per slot (device hooks)
 };
@@ -177,6 +178,7 @@ static int run(int argc, char **argv)
         else if (k == "--exit-after") a.exitAfter = (unsigned)std::stoul(val());
         else if (k == "--echoes") a.echoes = (unsigned)std::stoul(val());
         else if (k == "--flash-policy") a.flashPolicy = true;
+        else if (k == "--plain-accepter") a.plainAccepter = true;
         else if (k == "--device") a.device = std::stoi(val());
         else if (k == "--ring") a.ring = (unsigned)std::stoul(val());
         else {
@@ -226,6 +228,26 @@ static int run(int argc, char **argv)
         if (a.mode == "server") {
             std::printf("PORT %u\n", port);
             std::fflush(stdout);
+        }
+        if (a.plainAccepter) {
+            // Same engine, same event loop, same hooks object: sessions of this
+            // accepter have _rc4TcpEncryption == "" and must put plaintext on the
+            // wire (session.cpp:313-316, 496-499, 535-538, 603-606 are skipped).
+            AccepterID pID = mgr.addAccepter("127.0.0.1", 0);
+            SessionOptions &po = mgr.getAccepterOptions(pID)._sessionOptions;
+            po._rc4TcpEncryption.clear();
+            po._maxSendListCount = 40000;
+            po._onRawPacketProc = [](const TcpSessionPtr &s, const char *b, unsigned len) { s->send(b, len); };
+            po._onSessionLinked = [&](const TcpSessionPtr &) { linked++; };
+            po._onSessionClosed = [&](const TcpSessionPtr &) { closed++; };
+            if (!mgr.openAccepter(pID)) {
+                std::fprintf(stderr, "openAccepter (plain) failed\n");
+                return 1;
+            }
+            if (a.mode == "server") {
+                std::printf("PORT2 %u\n", (unsigned)mgr.getAccepterPort(pID));
+                std::fflush(stdout);
+            }
         }
     }
 

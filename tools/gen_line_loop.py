@@ -20,6 +20,11 @@ the lane's own session):
      (clamped to the sink when the session has no such block).
 Two halves (register sets P and Q) ping-pong; X is the transpose spare set.
 
+Stores are nt (the streamed lines stop competing for L2 with the S-box
+images: cfg5 306.6 -> 291.6 us, r01); loads use the default policy.  The
+whole-line-load variant (a second transpose) was 4 % slower and is only in
+git revision 849e847.
+
 The script also simulates the butterflies lane by lane with the DPP
 semantics used (quad_perm, row_shr:4, row_shl:4, bound_ctrl -> 0) and
 asserts that the result is the transpose.
@@ -157,7 +162,7 @@ def half(name: str, cur: int) -> str:
         w(q(f"v_cmp_gt_u32_e64 %[msk], v{LIM_BASE + qq}, %[sb]"))
         w(q(f"v_cndmask_b32_e64 v{sa}, v{SINK}, v{a}, %[msk]"))
         w(q(f"v_cndmask_b32_e64 v{sa + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
-        w(f'"global_store_dwordx4 v[{sa}:{sa + 1}], v[{final[qq]}:{final[qq] + 3}], off" ZRC4_LL_STP "\\n\\t"')
+        w(f'"global_store_dwordx4 v[{sa}:{sa + 1}], v[{final[qq]}:{final[qq] + 3}], off nt\\n\\t"')
     for qq in range(8):
         a = ADDR_BASE + 2 * qq
         w(q(f"v_lshl_add_u64 v[{a}:{a + 1}], 8, 4, v[{a}:{a + 1}]"))     # += 8 << 4 (shift must be 0..4)
@@ -170,13 +175,13 @@ def half(name: str, cur: int) -> str:
     w(q(f"v_cndmask_b32_e64 v{LA}, v{SINK}, %[palo], %[msk]"))
     w(q(f"v_cndmask_b32_e64 v{LA + 1}, v{SINK + 1}, %[pahi], %[msk]"))
     for d in range(4):
-        w(f'"global_load_dwordx4 v[{cur + 4 * d}:{cur + 4 * d + 3}], v[{LA}:{LA + 1}], off offset:{16 * d}" ZRC4_LDP "\\n\\t"')
+        w(f'"global_load_dwordx4 v[{cur + 4 * d}:{cur + 4 * d + 3}], v[{LA}:{LA + 1}], off offset:{16 * d}\\n\\t"')
     w(q("s_add_u32 %[s1], %[sb], 5"))
     w(q("v_cmp_lt_u32_e64 %[msk], %[s1], %[nblk]"))
     w(q(f"v_cndmask_b32_e64 v{LB}, v{SINK}, %[palo], %[msk]"))
     w(q(f"v_cndmask_b32_e64 v{LB + 1}, v{SINK + 1}, %[pahi], %[msk]"))
     for d in range(4):
-        w(f'"global_load_dwordx4 v[{cur + 16 + 4 * d}:{cur + 16 + 4 * d + 3}], v[{LB}:{LB + 1}], off offset:{64 + 16 * d}" ZRC4_LDP "\\n\\t"')
+        w(f'"global_load_dwordx4 v[{cur + 16 + 4 * d}:{cur + 16 + 4 * d + 3}], v[{LB}:{LB + 1}], off offset:{64 + 16 * d}\\n\\t"')
     w(q("v_add_co_u32_e32 %[palo], vcc, 0x80, %[palo]"))
     w(q("v_addc_co_u32_e32 %[pahi], vcc, 0, %[pahi], vcc"))
     w(q(f"LL_{name}L_%=:"))
@@ -184,74 +189,6 @@ def half(name: str, cur: int) -> str:
     w(q("s_cmp_ge_u32 %[sb], %[wmax]"))
     w(q("s_cbranch_scc1 LL_DONE_%="))
     return f"#define ZRC4_LL_HALF_{name} \\\n    " + " \\\n    ".join(out) + "\n"
-
-
-def half_coalesced(name: str, cur: int) -> str:
-    """Whole-line loads too: the line arrives as 8 loads of 8 lines each
-    (lane 8g+i: chunk i of session 8g+q's line in tuple q), a first transpose
-    gives every lane its own line, the keystream runs, a second transpose
-    turns it back for whole-line stores."""
-    start = {c: cur + 4 * c for c in range(8)}
-    ltl, lmap, lops, free = transpose_plan(start, [X_BASE + 4 * t for t in range(4)])
-    simulate(lops, start, lmap)
-    stl, smap, sops, _ = transpose_plan(lmap, free)
-    simulate(sops, lmap, smap)
-    q = lambda s: f'"{s}\\n\\t"'
-    out = []
-    w = out.append
-    # 1. this line's 8 loads: younger are the previous half's 8 stores and 8
-    #    loads -> vmcnt(16); the last half follows a half without loads: vmcnt(8)
-    w(q("s_add_u32 %[s1], %[sb], 2"))
-    w(q("s_cmp_ge_u32 %[s1], %[wmax]"))
-    w(q(f"s_cbranch_scc0 LC_{name}W_%="))
-    w(q("s_waitcnt vmcnt(8)"))
-    w(q(f"LC_{name}W_%=:"))
-    w(q("s_waitcnt vmcnt(16)"))
-    w(q("s_nop 1"))
-    for line in ltl:                                   # 2. lanes get their own line
-        w(q(line))
-    blk = lambda cs: "ZL_BLOCK(" + ", ".join(f"v{lmap[c] + d}" for c in cs for d in range(4)) + ")"
-    w(q("v_cmp_lt_u32_e64 %[msk], %[sb], %[nblk]"))     # 3. keystream, block b
-    w(q("s_and_b64 exec, %[full], %[msk]"))
-    w(q(f"s_cbranch_execz LC_{name}1_%="))
-    w(blk(range(4)))
-    w(q(f"LC_{name}1_%=:"))
-    w(q("s_add_u32 %[s1], %[sb], 1"))                  #    block b+1
-    w(q("v_cmp_lt_u32_e64 %[msk], %[s1], %[nblk]"))
-    w(q("s_and_b64 exec, %[full], %[msk]"))
-    w(q(f"s_cbranch_execz LC_{name}2_%="))
-    w(blk(range(4, 8)))
-    w(q(f"LC_{name}2_%=:"))
-    w(q("s_mov_b64 exec, %[full]"))
-    w(q("s_nop 4"))                                    # exec write -> DPP
-    for line in stl:                                   # 4. back to line-per-8-lanes
-        w(q(line))
-    for qq in range(8):                                # 5. whole-line stores
-        sa = SA0 if qq % 2 == 0 else SA1
-        a = ADDR_BASE + 2 * qq
-        w(q(f"v_cmp_gt_u32_e64 %[msk], v{LIM_BASE + qq}, %[sb]"))
-        w(q(f"v_cndmask_b32_e64 v{sa}, v{SINK}, v{a}, %[msk]"))
-        w(q(f"v_cndmask_b32_e64 v{sa + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
-        w(f'"global_store_dwordx4 v[{sa}:{sa + 1}], v[{smap[qq]}:{smap[qq] + 3}], off" ZRC4_LL_STP "\\n\\t"')
-    for qq in range(8):
-        a = ADDR_BASE + 2 * qq
-        w(q(f"v_lshl_add_u64 v[{a}:{a + 1}], 8, 4, v[{a}:{a + 1}]"))     # += 8 << 4 (shift must be 0..4)
-    # 6. whole-line loads of line b+4 (addresses now at line b+2: offset 128)
-    w(q("s_add_u32 %[s1], %[sb], 4"))
-    w(q("s_cmp_ge_u32 %[s1], %[wmax]"))
-    w(q(f"s_cbranch_scc1 LC_{name}L_%="))
-    for qq in range(8):
-        la = LA if qq % 2 == 0 else LB
-        a = ADDR_BASE + 2 * qq
-        w(q(f"v_cmp_gt_u32_e64 %[msk], v{LIM_BASE + qq}, %[s1]"))
-        w(q(f"v_cndmask_b32_e64 v{la}, v{SINK}, v{a}, %[msk]"))
-        w(q(f"v_cndmask_b32_e64 v{la + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
-        w(f'"global_load_dwordx4 v[{cur + 4 * qq}:{cur + 4 * qq + 3}], v[{la}:{la + 1}], off offset:128" ZRC4_LDP "\\n\\t"')
-    w(q(f"LC_{name}L_%=:"))
-    w(q("s_add_u32 %[sb], %[sb], 2"))
-    w(q("s_cmp_ge_u32 %[sb], %[wmax]"))
-    w(q("s_cbranch_scc1 LL_DONE_%="))
-    return f"#define ZRC4_LC_HALF_{name} \\\n    " + " \\\n    ".join(out) + "\n"
 
 
 def transpose_only(name: str, cur: int) -> str:
@@ -276,8 +213,6 @@ def main():
         "#pragma once\n",
         half("P", P_BASE),
         half("Q", Q_BASE),
-        half_coalesced("P", P_BASE),
-        half_coalesced("Q", Q_BASE),
         transpose_only("P", P_BASE),
     ]
     OUT.write_text("".join(text))

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Where a crypt_kernel launch spends its time, per wave (diagnostic build).
+
+Builds libzrc4 with ZRC4_TIMING=1 (zrc4_kernels.hpp, Stamps): lane 0 of every
+wave stamps s_memrealtime (100 MHz) and s_memtime (shader clock) at kernel
+entry (t0), S-boxes in LDS (t1), keystream done (t2) and state stored (t3).
+The last of --launches back-to-back launches (rotating over batches, as
+bench.py does) is read back and summarised:
+
+  prologue   t1 - t0   image + entries + LDS fill
+  chain      t2 - t1   the message loop (cycles per byte = clock delta / L)
+  epilogue   t3 - t2   x/y + image store, drained
+  span       max t3 - min t0 over the launch; entry skew = spread of t0
+
+  python tools/kernel_timeline.py --workloads cfg2,cfg3,65536x1024
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import statistics
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+SHAPES = {"cfg2": (4096, 1024), "cfg3": (65536, 256), "cfg4": (1024, 65536)}
+
+
+def summarise(rec: np.ndarray, waves: int, L: int) -> dict:
+    r = rec[:waves, :4].astype(np.float64) * 10.0 / 1000.0     # us (100 MHz ticks)
+    c = rec[:waves, 4:].astype(np.float64)
+    t0 = r[:, 0].min()
+    pro, chain, epi = r[:, 1] - r[:, 0], r[:, 2] - r[:, 1], r[:, 3] - r[:, 2]
+    clk = (c[:, 2] - c[:, 1]) / np.maximum(r[:, 2] - r[:, 1], 1e-9) / 1e3     # GHz
+    q = lambda a: {"min": round(float(a.min()), 3), "med": round(float(np.median(a)), 3),
+                   "max": round(float(a.max()), 3)}
+    return {"waves": waves, "span_us": round(float(r[:, 3].max() - t0), 3),
+            "entry_skew_us": q(r[:, 0] - t0), "prologue_us": q(pro), "chain_us": q(chain),
+            "epilogue_us": q(epi), "end_us": q(r[:, 3] - t0), "clock_ghz": q(clk),
+            "chain_cyc_per_byte": q((c[:, 2] - c[:, 1]) / max(L, 1))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workloads", default="cfg2,cfg3,65536x1024")
+    ap.add_argument("--launches", type=int, default=12)
+    ap.add_argument("--footprint-mib", type=int, default=640)
+    ap.add_argument("--build-only", action="store_true")
+    args = ap.parse_args()
+    from zsummerx_amd import build
+    path = build.build_variant("timing", {"ZRC4_TIMING": "1"})
+    if args.build_only:
+        print("built", path)
+        return
+    import torch
+    from zsummerx_amd import _capi, synth
+    lib = _capi.load(path)
+    lib.zrc4_debug_sink.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+    hip = C.CDLL("libamdhip64.so.7")          # the runtime torch already mapped (same SONAME)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    st = C.c_void_p(stream.cuda_stream)
+    out = {}
+    for wl in args.workloads.split(","):
+        S, L = SHAPES[wl] if wl in SHAPES else (int(v) for v in wl.lower().split("x"))
+        if S > 65536:
+            raise SystemExit("timing records cover at most 256 workgroups (65536 sessions)")
+        R = max(1, min(-(-args.footprint_mib * (1 << 20) // (S * (L + 256))), (1 << 24) // S))
+        n = S * R
+        keys = torch.from_numpy(synth.keys(0, n).reshape(-1)).to(dev)
+        adv = torch.from_numpy(synth.advance(0, n).view(np.int32)).to(dev)
+        klen = torch.full((n,), 16, dtype=torch.int32, device=dev)
+        koff = torch.arange(n, dtype=torch.int64, device=dev) * 16
+        pay = torch.from_numpy(synth.payload(0, n * L, threads=8)).to(dev)
+        off = torch.arange(n, dtype=torch.int64, device=dev) * L
+        ln = torch.full((n,), L, dtype=torch.int32, device=dev)
+        h = C.c_void_p()
+        _capi.check(lib.zrc4_create(C.byref(h), 0, n), "create")
+        _capi.check(lib.zrc4_ksa_range(h, 0, C.c_void_p(keys.data_ptr()), C.c_void_p(koff.data_ptr()),
+                                       C.c_void_p(klen.data_ptr()), n, st))
+        zoff = torch.zeros(n, dtype=torch.int64, device=dev)
+        scratch = torch.zeros(1000, dtype=torch.uint8, device=dev)
+        _capi.check(lib.zrc4_crypt(h, None, C.c_void_p(scratch.data_ptr()), C.c_void_p(zoff.data_ptr()),
+                                   C.c_void_p(adv.data_ptr()), n, st))
+        torch.cuda.synchronize()
+        for i in range(args.launches):
+            b = i % R
+            _capi.check(lib.zrc4_crypt_range(h, b * S, C.c_void_p(pay.data_ptr()),
+                                             C.c_void_p(off.data_ptr() + 8 * b * S),
+                                             C.c_void_p(ln.data_ptr() + 4 * b * S), S, st))
+        _capi.check(lib.zrc4_sync(h, st))
+        sink = C.c_void_p()
+        _capi.check(lib.zrc4_debug_sink(h, C.byref(sink)))
+        rec = np.zeros((1024, 8), dtype=np.uint64)
+        rc = hip.hipMemcpy(C.c_void_p(rec.ctypes.data), sink, C.c_size_t(rec.nbytes), 2)
+        if rc:
+            raise SystemExit(f"hipMemcpy failed {rc}")
+        waves = (S + 63) // 64
+        out[wl] = summarise(rec, waves, L)
+        print(wl, json.dumps(out[wl]), flush=True)
+        lib.zrc4_destroy(h)
+        del keys, adv, pay, off, ln, klen, koff, zoff
+        torch.cuda.empty_cache()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -98,6 +98,12 @@ class Context:
         check(self._lib.zrc4_crypt_range(self._h, int(first_slot), _ptr(payload), _ptr(off),
                                          _ptr(length), n, _stream(stream)), "zrc4_crypt_range")
 
+    def crypt_grouped(self, payload, off, length, ids, n=None, stream=None) -> None:
+        """zrc4_crypt_grouped: 256-entry buckets, each within one slot group."""
+        n = int(length.numel() if n is None else n)
+        check(self._lib.zrc4_crypt_grouped(self._h, _ptr(ids), _ptr(payload), _ptr(off), _ptr(length),
+                                           n, _stream(stream)), "zrc4_crypt_grouped")
+
     def xor_ring(self, ring, ring_cap: int, rid, pos, payload, off, length, n=None, stream=None) -> None:
         """zrc4_xor_ring: payload spans ^= keystream rings (consumed bytes zeroed)."""
         n = int(length.numel() if n is None else n)

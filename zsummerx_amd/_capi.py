@@ -19,7 +19,10 @@ ERRORS = {
     -4: "ZRC4_ERR_LAUNCH",
     -5: "ZRC4_ERR_SLOT_RANGE",
     -6: "ZRC4_ERR_HIP",
+    -7: "ZRC4_ERR_GROUP",
+    -8: "ZRC4_ERR_INTERNAL",
 }
+IDLE_SLOT = 0xFFFFFFFF
 
 # (name, restype, argtypes) for every symbol declared in include/zrc4.h
 _P = C.c_void_p
@@ -32,6 +35,7 @@ SIGNATURES = [
     ("zrc4_crypt", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_ksa_range", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_crypt_range", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P]),
+    ("zrc4_crypt_grouped", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_ksa_host", C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, C.c_uint32]),
     ("zrc4_crypt_host", C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, C.c_uint32]),
     ("zrc4_make_sbox", C.c_int, [_P, C.c_uint32, _P, C.c_size_t]),
@@ -78,6 +82,10 @@ def load(path: Path | str | None = None) -> C.CDLL:
             "there is no CPU fallback for the RC4 path")
     lib = C.CDLL(str(p))
     for name, res, args in SIGNATURES:
+        # an explicitly named A/B library from an older revision may predate
+        # an entry point; the product library must export every one
+        if path is not None and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

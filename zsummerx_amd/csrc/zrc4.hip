@@ -12,13 +12,6 @@
 #include <algorithm>
 #include <new>
 
-#ifndef ZRC4_PERSIST
-#define ZRC4_PERSIST 1
-#endif
-#ifndef ZRC4_WG_PER_CU
-#define ZRC4_WG_PER_CU 2     // persistent grid size per CU (A/B knob; LDS allows 2)
-#endif
-
 struct zrc4_ctx {
     int device;
     int num_cus;
@@ -27,9 +20,10 @@ struct zrc4_ctx {
     uint16_t *xy;           // per slot: x | y << 8
     uint8_t *sink;          // crypt_kernel's per-thread sink slots (loads/stores past a
                             // session's last block in the DPP line loop)
-    uint32_t *err;          // latched device-side fault bits, in pinned host memory:
-                            // kernels latch with a plain store, the host reads it
-                            // after the stream wait (no read-back copy)
+    uint32_t *err;          // latched device-side faults (zrc4::kErrWords words, one per
+                            // kind) in pinned host memory: kernels latch with a plain
+                            // store, the host reads them after the stream wait (no
+                            // read-back copy).  Per context, not per stream.
     // staging for the *_host entry points (grown on demand)
     uint8_t *d_stage;
     size_t d_stage_bytes;
@@ -72,46 +66,36 @@ int grow_stage(zrc4_ctx *c, size_t bytes)
 
 size_t align16(size_t v) { return (v + 15u) & ~(size_t)15u; }
 
-int launch_crypt(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, uint8_t *payload,
+// Kernel choice per launch: more 256-slot groups than CUs -> the persistent
+// throughput kernel (2 workgroups per CU, whole-line stores through the DPP
+// transpose); otherwise one group per workgroup (crypt_kernel: chain-bound,
+// per-lane stores).  A/B: the DPP path is 5-7 us slower at one group per CU
+// (cfg2 56.1 vs 48.8 us, cfg3 28.1 vs 22.7 us; profiles/r02_ab_dpp_direct.log).
+int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot, uint8_t *payload,
                  const uint64_t *off, const uint32_t *len, uint32_t n, hipStream_t s)
 {
     if (n == 0) return ZRC4_OK;
-    if (!ids && (uint64_t)first_slot + n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    if (mode == zrc4::kRange && (uint64_t)first_slot + n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
     const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
-#if ZRC4_STAGED_STORE >= 0
-    const bool staged = ZRC4_STAGED_STORE != 0;
-#else
-    const bool staged = grid > (uint32_t)c->num_cus;   // >1 workgroup per CU
-#endif
-#if ZRC4_STORE_PATH == 2
-    if (staged) {
-        // persistent over groups: 2 workgroups per CU (LDS- and VGPR-limited),
-        // each walking groups w, w + grid, ... (ZRC4_PERSIST=0: one group each)
-        const uint32_t wgs = ZRC4_PERSIST ? std::min(grid, (uint32_t)ZRC4_WG_PER_CU * (uint32_t)c->num_cus) : grid;
-        if (!ids && (first_slot & 255u) == 0u)
-            hipLaunchKernelGGL(zrc4::crypt_stream_kernel<true>, dim3(wgs), dim3(zrc4::kGroup), 0, s,
-                               c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
-                               c->err, c->sink);
+    const dim3 blk(zrc4::kGroup);
+    if (mode != zrc4::kGrouped && grid > (uint32_t)c->num_cus) {
+        const uint32_t wgs = std::min(grid, 2u * (uint32_t)c->num_cus);
+        if (mode == zrc4::kRange && (first_slot & 255u) == 0u)
+            hipLaunchKernelGGL(zrc4::crypt_stream_kernel<true>, dim3(wgs), blk, 0, s, c->arena, c->xy, ids,
+                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
         else
-            hipLaunchKernelGGL(zrc4::crypt_stream_kernel<false>, dim3(wgs), dim3(zrc4::kGroup), 0, s,
-                               c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
-                               c->err, c->sink);
-    } else
-#else
-    if (staged)
-        hipLaunchKernelGGL(zrc4::crypt_kernel<true>, dim3(grid), dim3(zrc4::kGroup), 0, s,
-                           c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
-                           c->err, c->sink);
-    else
-#endif
-    if (!ids)
-        hipLaunchKernelGGL((zrc4::crypt_kernel<false, true>), dim3(grid), dim3(zrc4::kGroup), 0, s,
-                           c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
-                           c->err, c->sink);
-    else
-        hipLaunchKernelGGL((zrc4::crypt_kernel<false, false>), dim3(grid), dim3(zrc4::kGroup), 0, s,
-                           c->arena, c->xy, ids, first_slot, payload, off, len, n, c->capacity,
-                           c->err, c->sink);
+            hipLaunchKernelGGL(zrc4::crypt_stream_kernel<false>, dim3(wgs), blk, 0, s, c->arena, c->xy, ids,
+                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
+    } else if (mode == zrc4::kRange) {
+        hipLaunchKernelGGL(zrc4::crypt_kernel<zrc4::kRange>, dim3(grid), blk, 0, s, c->arena, c->xy, ids,
+                           first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
+    } else if (mode == zrc4::kGrouped) {
+        hipLaunchKernelGGL(zrc4::crypt_kernel<zrc4::kGrouped>, dim3(grid), blk, 0, s, c->arena, c->xy, ids,
+                           first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
+    } else {
+        hipLaunchKernelGGL(zrc4::crypt_kernel<zrc4::kIds>, dim3(grid), blk, 0, s, c->arena, c->xy, ids,
+                           first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
+    }
     return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
 }
 
@@ -133,11 +117,12 @@ int check_err(zrc4_ctx *c, hipStream_t s)
 {
     ZRC4_TRY(hipStreamSynchronize(s));
     volatile uint32_t *e = c->err;
-    if (*e) {
-        *e = 0u;
-        return ZRC4_ERR_SLOT_RANGE;
-    }
-    return ZRC4_OK;
+    int rc = ZRC4_OK;
+    if (e[zrc4::kErrLdsLayout]) rc = ZRC4_ERR_INTERNAL;
+    else if (e[zrc4::kErrGroup]) rc = ZRC4_ERR_GROUP;
+    else if (e[zrc4::kErrSlotRange]) rc = ZRC4_ERR_SLOT_RANGE;
+    for (uint32_t i = 0; i < zrc4::kErrWords; ++i) e[i] = 0u;
+    return rc;
 }
 
 }  // namespace
@@ -167,12 +152,12 @@ int zrc4_create(zrc4_ctx **out, int device, uint32_t capacity)
     bool ok = hipMalloc(&c->arena, groups * (size_t)zrc4::kGroupBytes) == hipSuccess &&
               hipMalloc(&c->xy, (size_t)c->capacity * sizeof(uint16_t)) == hipSuccess &&
               hipMalloc(&c->sink, zrc4::kSinkBytes) == hipSuccess &&
-              hipHostMalloc(&c->err, sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc(&c->err, zrc4::kErrWords * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
               hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     if (!ok) { zrc4_destroy(c); return ZRC4_ERR_OUT_OF_MEMORY; }
     // Fresh slots hold the reference's empty-key state: identity box, x = y = 0
     // (what makeSBox("") produces, rc4_encryption.h:48-53).
-    *c->err = 0u;
+    for (uint32_t i = 0; i < zrc4::kErrWords; ++i) c->err[i] = 0u;
     hipLaunchKernelGGL(zrc4::identity_kernel, dim3((unsigned)groups), dim3(zrc4::kGroup), 0,
                        c->stream, c->arena);
     if (hipGetLastError() != hipSuccess ||
@@ -220,7 +205,7 @@ int zrc4_crypt(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_
     if (n && (!payload || !off || !len)) return ZRC4_ERR_INVALID_ARG;
     int rc = set_device(c);
     if (rc) return rc;
-    return launch_crypt(c, ids, 0, payload, off, len, n, (hipStream_t)stream);
+    return launch_crypt(c, ids ? zrc4::kIds : zrc4::kRange, ids, 0, payload, off, len, n, (hipStream_t)stream);
 }
 
 int zrc4_ksa_range(zrc4_ctx *c, uint32_t first_slot, const uint8_t *keys,
@@ -240,7 +225,17 @@ int zrc4_crypt_range(zrc4_ctx *c, uint32_t first_slot, uint8_t *payload, const u
     if (n && (!payload || !off || !len)) return ZRC4_ERR_INVALID_ARG;
     int rc = set_device(c);
     if (rc) return rc;
-    return launch_crypt(c, nullptr, first_slot, payload, off, len, n, (hipStream_t)stream);
+    return launch_crypt(c, zrc4::kRange, nullptr, first_slot, payload, off, len, n, (hipStream_t)stream);
+}
+
+int zrc4_crypt_grouped(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_t *off,
+                       const uint32_t *len, uint32_t n, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n && (!ids || !payload || !off || !len)) return ZRC4_ERR_INVALID_ARG;
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_crypt(c, zrc4::kGrouped, ids, 0, payload, off, len, n, (hipStream_t)stream);
 }
 
 int zrc4_xor_ring(zrc4_ctx *c, uint8_t *ring, uint32_t ring_cap, const uint32_t *rid,
@@ -329,7 +324,7 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
     memcpy(c->h_stage + o_len, len, (size_t)n * 4);
     if (payload_bytes) memcpy(c->h_stage + o_pay, payload, payload_bytes);
     ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
-    rc = launch_crypt(c, ids ? (const uint32_t *)(c->d_stage + o_ids) : nullptr, 0,
+    rc = launch_crypt(c, ids ? zrc4::kIds : zrc4::kRange, ids ? (const uint32_t *)(c->d_stage + o_ids) : nullptr, 0,
                       c->d_stage + o_pay, (const uint64_t *)(c->d_stage + o_off),
                       (const uint32_t *)(c->d_stage + o_len), n, c->stream);
     if (rc) return rc;
@@ -411,10 +406,23 @@ const char *zrc4_strerror(int code)
     case ZRC4_ERR_LAUNCH: return "kernel launch failed";
     case ZRC4_ERR_SLOT_RANGE: return "slot id out of range (>= capacity)";
     case ZRC4_ERR_HIP: return "HIP runtime error";
+    case ZRC4_ERR_GROUP: return "zrc4_crypt_grouped: a 256-entry bucket mixes slot groups";
+    case ZRC4_ERR_INTERNAL: return "internal error: S-box image not at LDS offset 0";
     default: return "unknown zrc4 error";
     }
 }
 
-const char *zrc4_version(void) { return "zrc4-mi355x 0.1 (gfx950)"; }
+const char *zrc4_version(void) { return "zrc4-mi355x 0.2 (gfx950)"; }
+
+#if ZRC4_TIMING
+// Diagnostic builds only: the per-wave timestamp records (zrc4_kernels.hpp,
+// Stamps) live in the context's sink buffer.
+int zrc4_debug_sink(zrc4_ctx *c, void **out)
+{
+    if (!c || !out) return ZRC4_ERR_INVALID_ARG;
+    *out = c->sink;
+    return ZRC4_OK;
+}
+#endif
 
 }  // extern "C"

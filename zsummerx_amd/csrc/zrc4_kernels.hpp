@@ -2,7 +2,12 @@
 //
 // Reference algorithm: /root/reference/depends/rc4/rc4_encryption.h
 //   makeSBox   :46-72  -> ksa_kernel
-//   encryption :74-93  -> crypt_kernel
+//   encryption :74-93  -> crypt_kernel (<= 1 group per CU), crypt_stream_kernel
+//
+// Only the instantiated product paths live here.  The round-1 A/B variants
+// (LDS-staged quad / line stores, whole-line loads, step-order, stagger,
+// ablation and cache-policy knobs) are reproducible from git revision 849e847
+// with tools/ab_bench.py --variant name@849e847:KNOB=v.
 //
 // Work decomposition
 //   One lane = one RC4 stream (slot).  RC4 is serial inside a stream (each
@@ -19,6 +24,9 @@
 //      32 distinct banks for ANY indices k (conflict-free), and every address
 //      is a 16-bit value whose top byte is the S-box index, so x/y/t updates
 //      are single 16-bit adds (wrap mod 256 for free).
+//   The hand-written steps use these addresses as ABSOLUTE LDS addresses, so
+//   the S-box image must sit at LDS offset 0 of the workgroup; every kernel
+//   checks that at entry (lds_base_ok) and latches kErrLdsLayout otherwise.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,14 +36,29 @@ namespace zrc4 {
 constexpr int kGroup = 256;            // slots per workgroup / arena group
 constexpr int kGroupBytes = 256 * 256; // 64 KiB S-box image per group
 
-enum : uint32_t { kErrSlotRange = 1u };
+// Fault latch: words in pinned host memory, one per fault kind; every
+// faulting lane stores 1 with a plain system-scope store (no read-modify-
+// write), the host reads and clears them after its stream wait (zrc4_sync).
+enum : uint32_t {
+    kErrSlotRange = 0,   // a slot id >= capacity (entry skipped)
+    kErrLdsLayout = 1,   // the S-box image is not at LDS offset 0 (launch skipped)
+    kErrGroup = 2,       // zrc4_crypt_grouped: a bucket mixes slot groups (bucket skipped)
+    kErrWords = 4,
+};
 
-// The fault latch lives in pinned host memory; every faulting lane stores the
-// same value, so a plain (non-atomic) system-visible store is enough and the
-// host reads it after its stream wait.
-__device__ __forceinline__ void latch_fault(uint32_t *err)
+__device__ __forceinline__ void latch_fault(uint32_t *err, uint32_t kind)
 {
-    __hip_atomic_store(err, kErrSlotRange, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(err + kind, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The asm addresses S-box bytes absolutely (no base register): S must be the
+// workgroup's first LDS byte.  (uint32_t) of a generic LDS pointer is its
+// offset inside the LDS aperture.
+__device__ __forceinline__ bool lds_base_ok(const uint8_t *S, uint32_t *err)
+{
+    if ((uint32_t)(uintptr_t)S == 0u) return true;
+    if (threadIdx.x == 0) latch_fault(err, kErrLdsLayout);
+    return false;
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -47,9 +70,42 @@ __device__ __forceinline__ uint32_t col_of(uint32_t j)
 }
 
 // ---------------------------------------------------------------------------
+// Diagnostic timing build (ZRC4_TIMING=1, never the product): lane 0 of each
+// wave stamps s_memrealtime (100 MHz) and s_memtime (shader clock) at kernel
+// entry, S-boxes in LDS, keystream done, and state stored; the 64-byte record
+// of wave w of workgroup b goes to sink + ((b * 4 + w) & 1023) * 64
+// (zrc4_debug_sink exports the sink in such builds; tools/kernel_timeline.py).
+// ---------------------------------------------------------------------------
+#ifndef ZRC4_TIMING
+#define ZRC4_TIMING 0
+#endif
+struct Stamps {
+    uint64_t r[4], c[4];
+};
+__device__ __forceinline__ void stamp(Stamps &s, int i)
+{
+#if ZRC4_TIMING
+    s.r[i] = __builtin_amdgcn_s_memrealtime();
+    s.c[i] = __builtin_amdgcn_s_memtime();
+#endif
+}
+__device__ __forceinline__ void stamps_out(const Stamps &s, uint8_t *sink)
+{
+#if ZRC4_TIMING
+    if ((threadIdx.x & 63u) == 0u) {
+        uint64_t *o = reinterpret_cast<uint64_t *>(sink + (((blockIdx.x * 4u + (threadIdx.x >> 6)) & 1023u) * 64u));
+        for (int i = 0; i < 4; ++i) {
+            o[i] = s.r[i];
+            o[4 + i] = s.c[i];
+        }
+    }
+#endif
+}
+
+// ---------------------------------------------------------------------------
 // Group state load / store.
-//   fast: the workgroup's 256 entries are exactly slots g*256 .. g*256+255
-//         (or ids == NULL): copy the 64 KiB image as 16 B per lane, coalesced.
+//   fast: the workgroup owns one whole 256-slot group: copy the 64 KiB image
+//         as 16 B per lane, coalesced.
 //   slow: arbitrary slot ids: each lane gathers its own 256 bytes (strided).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void image_to_lds(uint8_t *lds, const uint8_t *img)
@@ -66,16 +122,6 @@ __device__ __forceinline__ void lds_to_image(uint8_t *img, const uint8_t *lds)
     uint4 *dst = reinterpret_cast<uint4 *>(img);
 #pragma unroll
     for (int i = 0; i < 16; ++i) dst[i * 256 + threadIdx.x] = src[i * 256 + threadIdx.x];
-}
-
-// Same copy with nontemporal (nt) stores: the image is not read again in
-// this launch, so it need not compete for L2 (A/B knob ZRC4_IMG_NT).
-__device__ __forceinline__ void lds_to_image_nt(uint8_t *img, const uint8_t *lds)
-{
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(lds);
-    u32x4 *dst = reinterpret_cast<u32x4 *>(img);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) __builtin_nontemporal_store(src[i * 256 + threadIdx.x], &dst[i * 256 + threadIdx.x]);
 }
 
 __device__ __forceinline__ void gather_column(uint8_t *lds, uint32_t col,
@@ -113,6 +159,22 @@ __device__ __forceinline__ void scatter_column(uint8_t *arena, uint32_t slot,
 struct Rc4Lane {
     uint32_t x0, a0, ya, ta, x1, col;
 };
+
+__device__ __forceinline__ void lane_init(Rc4Lane &st, const uint8_t *S, uint32_t col, uint32_t sxy)
+{
+    const uint32_t x = sxy & 255u, y = (sxy >> 8) & 255u;
+    st.col = col;
+    st.x0 = (((x + 1u) & 255u) << 8) | col;
+    st.a0 = S[st.x0];
+    st.ya = (y << 8) | col;
+    st.ta = col;
+    st.x1 = col;
+}
+
+__device__ __forceinline__ uint16_t lane_xy(const Rc4Lane &st)
+{
+    return (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
+}
 
 // Portable C step with the same state layout (head/tail bytes, 16-B chunks).
 __device__ __forceinline__ uint32_t prga_step(uint8_t *S, Rc4Lane &st)
@@ -157,30 +219,9 @@ __device__ __forceinline__ uint4 xor16(uint8_t *S, Rc4Lane &st, uint4 v)
 // (ds_read_u8_d16_hi does NOT preserve the low half on gfx950 -- measured --
 // so keystream bytes are not packed through d16 loads.)
 //
-// Registers: XC = address of S[x] for this step, XN = address of S[x+1]
-// (computed one step ahead, so only  y+=a -> read b -> write a -> read S[x+1]
-// sit between S[x+1] arriving and the next S[x+1] read being issued).  XC is
-// free after the S[x] = b write and becomes x+2 (the next step's XN).
+// XC = address of S[x] for this step; XN = address of S[x+1], derived from XC
+// inside the step right before its read.  XC is free after the S[x] = b write.
 // Per byte: 4 VALU + 5 LDS + 2 waits.
-#ifndef ZRC4_STEP_ORDER
-#define ZRC4_STEP_ORDER 1
-#endif
-#if ZRC4_STEP_ORDER == 2
-#define ZRC4_CORE(XC, XN, A, P, K)                                                               \
-    "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
-    "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
-    "ds_read_u8 %[b], %[ya]\n\t"                                                                 \
-    "ds_write_b8 %[ya], %[" #A "]\n\t"                                                           \
-    "ds_read_u8 %[" #P "], %[" #XN "]\n\t"                                                       \
-    "s_waitcnt lgkmcnt(2)\n\t"                                                                   \
-    "ds_write_b8 %[" #XC "], %[b]\n\t"                                                           \
-    "v_add_u32_sdwa %[ta], %[" #A "], %[b] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "           \
-    "src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"                                                        \
-    "ds_read_u8 %[" #K "], %[ta]\n\t"                                                            \
-    "v_add_u32_sdwa %[" #XC "], 1, %[" #XN "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "        \
-    "src0_sel:DWORD src1_sel:BYTE_1\n\t"                                                         \
-    "s_waitcnt lgkmcnt(2)\n\t"
-#else  // order 1: x+1 computed inside the step (XN derived from XC before the read)
 #define ZRC4_CORE(XC, XN, A, P, K)                                                               \
     "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
     "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
@@ -195,65 +236,16 @@ __device__ __forceinline__ uint4 xor16(uint8_t *S, Rc4Lane &st, uint4 v)
     "src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"                                                        \
     "ds_read_u8 %[" #K "], %[ta]\n\t"                                                            \
     "s_waitcnt lgkmcnt(2)\n\t"
-#endif
-#if ZRC4_STEP_ORDER == 2
-#define ZRC4_X1_INIT                                                                             \
-    "v_add_u32_sdwa %[x1], 1, %[x0] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "                  \
-    "src0_sel:DWORD src1_sel:BYTE_1\n\t"
-#else
-#define ZRC4_X1_INIT ""
-#endif
-
-#define ZRC4_XOR(D, SEL, K)                                                                      \
-    "v_xor_b32_sdwa %[" #D "], %[" #D "], %[" #K "] dst_sel:" #SEL                               \
-    " dst_unused:UNUSED_PRESERVE src0_sel:" #SEL " src1_sel:BYTE_0\n\t"
 
 #define ZRC4_E ZRC4_CORE(x0, x1, a0, a1, k0)   // even step: keystream -> k0
 #define ZRC4_O ZRC4_CORE(x1, x0, a1, a0, k1)   // odd step:  keystream -> k1
-#define ZRC4_W0(D)                                                                               \
-    ZRC4_E ZRC4_O ZRC4_XOR(D, BYTE_0, k0) ZRC4_E ZRC4_XOR(D, BYTE_1, k1)                        \
-    ZRC4_O ZRC4_XOR(D, BYTE_2, k0)
-#define ZRC4_W(DP, D)                                                                            \
-    ZRC4_E ZRC4_XOR(DP, BYTE_3, k1) ZRC4_O ZRC4_XOR(D, BYTE_0, k0)                              \
-    ZRC4_E ZRC4_XOR(D, BYTE_1, k1) ZRC4_O ZRC4_XOR(D, BYTE_2, k0)
-
-// 64 keystream bytes XORed into d[0..15] (little-endian dwords).  On entry
-// st.x0 / st.a0 / st.ya hold the C-step state; x1 (byte 0 = col) is derived
-// here.  On exit every asm output has landed (final lgkmcnt(0)).
-__device__ __forceinline__ void xor64_asm(Rc4Lane &st, uint4 (&q)[4])
-{
-    uint32_t b, k0, k1, a1;
-    asm volatile(
-        ZRC4_X1_INIT
-        ZRC4_W0(d0) ZRC4_W(d0, d1) ZRC4_W(d1, d2) ZRC4_W(d2, d3)
-        ZRC4_W(d3, d4) ZRC4_W(d4, d5) ZRC4_W(d5, d6) ZRC4_W(d6, d7)
-        ZRC4_W(d7, d8) ZRC4_W(d8, d9) ZRC4_W(d9, d10) ZRC4_W(d10, d11)
-        ZRC4_W(d11, d12) ZRC4_W(d12, d13) ZRC4_W(d13, d14) ZRC4_W(d14, d15)
-        "s_waitcnt lgkmcnt(0)\n\t"
-        ZRC4_XOR(d15, BYTE_3, k1)
-        : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1),
-          [a0] "+v"(st.a0), [a1] "=&v"(a1), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
-          [d0] "+v"(q[0].x), [d1] "+v"(q[0].y), [d2] "+v"(q[0].z), [d3] "+v"(q[0].w),
-          [d4] "+v"(q[1].x), [d5] "+v"(q[1].y), [d6] "+v"(q[1].z), [d7] "+v"(q[1].w),
-          [d8] "+v"(q[2].x), [d9] "+v"(q[2].y), [d10] "+v"(q[2].z), [d11] "+v"(q[2].w),
-          [d12] "+v"(q[3].x), [d13] "+v"(q[3].y), [d14] "+v"(q[3].z), [d15] "+v"(q[3].w)
-        :
-        : "memory");
-}
 
 // 64-byte blocks are kept as uint4[4] so every 16 bytes sits in an aligned
-// 4-register tuple (one dwordx4 each); as uint32_t[16] the register allocator
-// placed them off-tuple and hipcc split the loads into dwordx2/dwordx4 pieces.
+// 4-register tuple (one dwordx4 each).
 __device__ __forceinline__ void load64(uint4 (&q)[4], const uint4 *p)
 {
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = p[i];
-}
-
-__device__ __forceinline__ void store64(uint4 *p, const uint4 (&q)[4])
-{
-#pragma unroll
-    for (int i = 0; i < 4; ++i) p[i] = q[i];
 }
 
 // Bytes before the first 16-byte boundary of a message (<= len).
@@ -271,59 +263,22 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
 //   * payload blocks ping-pong between two PINNED register tuples,
 //     A = v40..v55 and B = v56..v71, so the dwordx4 loads/stores and the
 //     per-byte SDWA xors name the same registers;
-//   * the next block is prefetched under an exec mask of the lanes that have
-//     one; one s_waitcnt vmcnt(8) per block (in-order VMEM completion: the
-//     8 younger ops are the previous block's stores and this prefetch);
+//   * the next block's four loads go out under the loop's full exec (a lane
+//     with no next block re-reads its current block), so every vmcnt wait is
+//     a static count; one s_waitcnt vmcnt(8) per block (in-order VMEM
+//     completion: the 8 younger ops are the previous block's stores and this
+//     prefetch);
 //   * exec shrinks as lanes run out of blocks (ragged batches), and is
-//     restored on exit.  Lanes keep their own pointer and RC4 state.
-// On entry A holds block 0 (landed), nblk >= 1 for every active lane.
+//     restored on exit.  Lanes keep their own pointer and RC4 state;
+//   * block 0 runs its keystream AHEAD of its payload (ZL_FIRST): the 64
+//     keystream bytes go into K = v72..v87 (cleared) and only then does the
+//     wave wait for block 0's loads -- vmcnt(4): block 1's four prefetch
+//     loads are the only younger VMEM ops -- and XOR K into A.  The caller
+//     issues block 0 from asm (issue_block_asm) before the LDS fill, so its
+//     HBM round trip overlaps the fill and 64 PRGA steps.
+// On entry A holds (or is loading) block 0, nblk >= 1 for every active lane.
+// Cache policy: plain loads and stores (nt stores cost cfg3 +2.7 %, r01).
 // ---------------------------------------------------------------------------
-// Cache policy of the payload stores / loads issued from asm.
-//   ZRC4_STP_MODE (direct path) / ZRC4_LL_STP_MODE (throughput line loop):
-//     0 plain, 1 sc1, 2 nt, 3 sc0 sc1;   ZRC4_LDP_MODE (both): 0 plain, 1 nt, 2 sc1
-// Measured back to back (profiles/r01_ab_cache_policy.log): nt stores take
-// cfg5 from 306.6 to 291.6 us (the streamed lines stop competing for L2) but
-// cost cfg3 +2.7 %; sc1 / sc0 sc1 stores and nt loads are slower.
-#ifndef ZRC4_STP_MODE
-#define ZRC4_STP_MODE 0
-#endif
-#ifndef ZRC4_IMG_NT
-#define ZRC4_IMG_NT 0
-#endif
-#ifndef ZRC4_DIRECT_IMG_NT
-#define ZRC4_DIRECT_IMG_NT 0   // crypt_kernel's epilogue image store with nt (A/B knob)
-#endif
-#ifndef ZRC4_LL_STP_MODE
-#define ZRC4_LL_STP_MODE 2
-#endif
-#if ZRC4_LL_STP_MODE == 1
-#define ZRC4_LL_STP " sc1"
-#elif ZRC4_LL_STP_MODE == 2
-#define ZRC4_LL_STP " nt"
-#elif ZRC4_LL_STP_MODE == 3
-#define ZRC4_LL_STP " sc0 sc1"
-#else
-#define ZRC4_LL_STP ""
-#endif
-#ifndef ZRC4_LDP_MODE
-#define ZRC4_LDP_MODE 0
-#endif
-#if ZRC4_STP_MODE == 1
-#define ZRC4_STP " sc1"
-#elif ZRC4_STP_MODE == 2
-#define ZRC4_STP " nt"
-#elif ZRC4_STP_MODE == 3
-#define ZRC4_STP " sc0 sc1"
-#else
-#define ZRC4_STP ""
-#endif
-#if ZRC4_LDP_MODE == 1
-#define ZRC4_LDP " nt"
-#elif ZRC4_LDP_MODE == 2
-#define ZRC4_LDP " sc1"
-#else
-#define ZRC4_LDP ""
-#endif
 #define ZL_XOR(R, SEL, K)                                                                        \
     "v_xor_b32_sdwa " #R ", " #R ", %[" #K "] dst_sel:" #SEL                                     \
     " dst_unused:UNUSED_PRESERVE src0_sel:" #SEL " src1_sel:BYTE_0\n\t"
@@ -348,25 +303,23 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
 #define ZL_B2 "v[64:67]"
 #define ZL_B3 "v[68:71]"
 // Next block's four loads into R: from pa + 64, or -- for lanes with no next
-// block -- a harmless re-read of the current block (pa), always under the
-// loop's full exec, so every wait below counts a fixed number of VMEM ops
-// whether or not the hardware would issue an exec == 0 load.
-// pa = v[88:89], pn = v[90:91].
+// block -- a harmless re-read of the current block (pa).  pa = v[88:89],
+// pn = v[90:91].
 #define ZL_PREFETCH(R0, R1, R2, R3)                                                              \
     "s_add_u32 %[i1], %[i], 1\n\t"                                                               \
     "v_cmp_lt_u32_e32 vcc, %[i1], %[nblk]\n\t"                                                   \
     "v_lshl_add_u64 v[90:91], v[88:89], 0, 64\n\t"                                               \
     "v_cndmask_b32_e32 v90, v88, v90, vcc\n\t"                                                   \
     "v_cndmask_b32_e32 v91, v89, v91, vcc\n\t"                                                   \
-    "global_load_dwordx4 " R0 ", v[90:91], off" ZRC4_LDP "\n\t"                                  \
-    "global_load_dwordx4 " R1 ", v[90:91], off offset:16" ZRC4_LDP "\n\t"                        \
-    "global_load_dwordx4 " R2 ", v[90:91], off offset:32" ZRC4_LDP "\n\t"                        \
-    "global_load_dwordx4 " R3 ", v[90:91], off offset:48" ZRC4_LDP "\n\t"
+    "global_load_dwordx4 " R0 ", v[90:91], off\n\t"                                              \
+    "global_load_dwordx4 " R1 ", v[90:91], off offset:16\n\t"                                    \
+    "global_load_dwordx4 " R2 ", v[90:91], off offset:32\n\t"                                    \
+    "global_load_dwordx4 " R3 ", v[90:91], off offset:48\n\t"
 #define ZL_STORE(R0, R1, R2, R3)                                                                 \
-    "global_store_dwordx4 v[88:89], " R0 ", off" ZRC4_STP "\n\t"                                 \
-    "global_store_dwordx4 v[88:89], " R1 ", off offset:16" ZRC4_STP "\n\t"                       \
-    "global_store_dwordx4 v[88:89], " R2 ", off offset:32" ZRC4_STP "\n\t"                       \
-    "global_store_dwordx4 v[88:89], " R3 ", off offset:48" ZRC4_STP "\n\t"                       \
+    "global_store_dwordx4 v[88:89], " R0 ", off\n\t"                                             \
+    "global_store_dwordx4 v[88:89], " R1 ", off offset:16\n\t"                                   \
+    "global_store_dwordx4 v[88:89], " R2 ", off offset:32\n\t"                                   \
+    "global_store_dwordx4 v[88:89], " R3 ", off offset:48\n\t"                                   \
     "v_lshl_add_u64 v[88:89], v[88:89], 0, 64\n\t"                                               \
     "s_add_u32 %[i], %[i], 1\n\t"
 #define ZL_ACTIVE                                                                                \
@@ -385,14 +338,6 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
     "s_waitcnt vmcnt(8)\n\t"                                                                     \
     ZL_BLOCK(v56, v57, v58, v59, v60, v61, v62, v63, v64, v65, v66, v67, v68, v69, v70, v71)    \
     ZL_STORE(ZL_B0, ZL_B1, ZL_B2, ZL_B3)
-
-// Block 0 with its keystream generated AHEAD of its payload (ZRC4_LEAD=1):
-// the 64 keystream bytes go into K = v72..v87 (cleared), and only then does
-// the wave wait for block 0's loads -- vmcnt(4): block 1's four prefetch
-// loads are the only younger VMEM ops -- and XOR K into A.  When the caller
-// issued block 0 from asm right before the LDS fill (issue_block_asm), its
-// HBM round trip overlaps 64 PRGA steps instead of stalling the wave at the
-// top of the loop (hipcc drained it with a vmcnt(0) there).
 #define ZL_FIRST                                                                                 \
     "s_mov_b32 %[i], 0\n\t"                                                                      \
     ZL_PREFETCH(ZL_B0, ZL_B1, ZL_B2, ZL_B3)                                                      \
@@ -412,9 +357,6 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
     "v_xor_b32_e32 v54, v54, v86\n\tv_xor_b32_e32 v55, v55, v87\n\t"                               \
     ZL_STORE(ZL_A0, ZL_A1, ZL_A2, ZL_A3)                                                         \
     "s_branch ZL_MID_%=\n\t"
-#ifndef ZRC4_LEAD
-#define ZRC4_LEAD 1
-#endif
 
 __device__ __forceinline__ void crypt_blocks_asm(Rc4Lane &st, uint4 *&p, uint32_t nblk,
                                                  const uint4 (&A)[4])
@@ -426,11 +368,7 @@ __device__ __forceinline__ void crypt_blocks_asm(Rc4Lane &st, uint4 *&p, uint32_
     uint32_t i, i1, b, k0, k1, a1s;
     asm volatile(
         "s_mov_b64 %[save], exec\n\t"
-#if ZRC4_LEAD
         ZL_FIRST
-#else
-        "s_mov_b32 %[i], 0\n\t"
-#endif
         "ZL_LOOP_%=:\n\t"
         ZL_HALF_A
         "ZL_MID_%=:\n\t"
@@ -453,13 +391,12 @@ __device__ __forceinline__ void crypt_blocks_asm(Rc4Lane &st, uint4 *&p, uint32_
 // neither counts nor waits for it (crypt_blocks_asm's lead block does).
 __device__ __forceinline__ void issue_block_asm(uint4 (&A)[4], const uint8_t *msg)
 {
-#if ZRC4_LEAD
     u32x4 a0, a1, a2, a3;
     asm volatile(
-        "global_load_dwordx4 v[40:43], %[p], off" ZRC4_LDP "\n\t"
-        "global_load_dwordx4 v[44:47], %[p], off offset:16" ZRC4_LDP "\n\t"
-        "global_load_dwordx4 v[48:51], %[p], off offset:32" ZRC4_LDP "\n\t"
-        "global_load_dwordx4 v[52:55], %[p], off offset:48" ZRC4_LDP "\n\t"
+        "global_load_dwordx4 v[40:43], %[p], off\n\t"
+        "global_load_dwordx4 v[44:47], %[p], off offset:16\n\t"
+        "global_load_dwordx4 v[48:51], %[p], off offset:32\n\t"
+        "global_load_dwordx4 v[52:55], %[p], off offset:48\n\t"
         : "=&{v[40:43]}"(a0), "=&{v[44:47]}"(a1), "=&{v[48:51]}"(a2), "=&{v[52:55]}"(a3)
         : [p] "v"(msg)
         : "memory");
@@ -467,19 +404,11 @@ __device__ __forceinline__ void issue_block_asm(uint4 (&A)[4], const uint8_t *ms
     A[1] = make_uint4(a1[0], a1[1], a1[2], a1[3]);
     A[2] = make_uint4(a2[0], a2[1], a2[2], a2[3]);
     A[3] = make_uint4(a3[0], a3[1], a3[2], a3[3]);
-#else
-    load64(A, reinterpret_cast<const uint4 *>(msg));
-#endif
 }
 
-#ifndef ZRC4_ASM_LOOP
-#define ZRC4_ASM_LOOP 1      // 0: per-block asm statements with hipcc's loop (A/B builds)
-#endif
-
 // Crypt one lane's message in place: unaligned head bytes, 64-byte blocks
-// (hand-written step; the next block's loads are issued before the current
-// block's keystream), 16-byte chunks, tail bytes.  If `pre` is set, A already
-// holds the first 64-byte block (loaded by the caller ahead of the LDS fill).
+// (crypt_blocks_asm), 16-byte chunks, tail bytes.  If `pre` is set, A already
+// holds the first 64-byte block (issued by the caller ahead of the LDS fill).
 __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st, uint8_t *msg,
                                               uint32_t len, uint4 (&A)[4], bool pre)
 {
@@ -490,30 +419,9 @@ __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st, uint8_t *
 
     uint4 *p = reinterpret_cast<uint4 *>(msg);
     const uint32_t nblk = len >> 6;
-    if (ZRC4_ASM_LOOP && nblk) {
+    if (nblk) {
         if (!pre) issue_block_asm(A, reinterpret_cast<const uint8_t *>(p));
         crypt_blocks_asm(st, p, nblk, A);
-    } else if (nblk) {
-        // Ping-pong buffers A/B, no loop-carried copies, and the next block's
-        // four loads issued unconditionally (re-reading the current block when
-        // there is none) so the compiler's vmcnt waits stay counted and never
-        // drain the prefetch.
-        uint4 B[4];
-        if (!pre) load64(A, p);
-        uint32_t i = 0;
-        while (true) {
-            load64(B, (i + 1 < nblk) ? p + 4 : p);
-            xor64_asm(st, A);
-            store64(p, A);
-            if (++i == nblk) break;
-            p += 4;
-            load64(A, (i + 1 < nblk) ? p + 4 : p);
-            xor64_asm(st, B);
-            store64(p, B);
-            if (++i == nblk) break;
-            p += 4;
-        }
-        p += 4;
     }
     uint32_t rem = len & 63u;
     while (rem >= 16u) {
@@ -524,22 +432,6 @@ __device__ __forceinline__ void crypt_message(uint8_t *S, Rc4Lane &st, uint8_t *
     uint8_t *t = reinterpret_cast<uint8_t *>(p);
     for (uint32_t i = 0; i < rem; ++i) t[i] ^= (uint8_t)prga_step(S, st);
 }
-
-// Store path per launch (host picks, zrc4.hip): staged stores pay off when
-// two workgroups share a CU (store-throughput bound); with one wave per SIMD
-// the kernel is chain-latency bound and the staging round trip costs more.
-// ZRC4_STAGED_STORE=0/1 forces one path for A/B builds.
-#ifndef ZRC4_STAGED_STORE
-#define ZRC4_STAGED_STORE -1
-#endif
-
-constexpr int kStageBytes = 4096;                  // per wave: one 64-B block per lane
-constexpr int kSmemBytes = kGroupBytes + 4 * kStageBytes;   // 80 KiB: 2 workgroups per CU
-
-// global-address-space views (pointers rebuilt from shuffled integers would
-// otherwise become flat accesses, which force vmcnt(0)+lgkmcnt(0) waits)
-typedef __attribute__((address_space(1))) uint8_t gu8;
-typedef __attribute__((address_space(1))) u32x4 gu32x4;
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 {
@@ -551,262 +443,24 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
     return v;
 }
 
-// Staged-store message loop (the default).
-//
-// Measured on gfx950 (tools/ubench/lds_ubench.hip, 8 waves/CU): per-lane
-// scattered 16-B loads stream at 5.5 TB/s, but per-lane scattered 16-B
-// STORES (64 lines per wave-instruction) at only 0.96 TB/s, against 2.4 TB/s
-// when each 4-lane quad writes 64 contiguous bytes.  So loads stay per lane
-// (prefetched one block ahead in registers) while results go through a
-// 4 KiB per-wave LDS staging slot and leave as quad-coalesced stores: lane l
-// of store instruction q writes 16 B of session 16q + l/4.  The block loop is
-// wave-uniform (to the wave's longest message) so every lane can store on
-// behalf of others; owner lanes past their own end skip the keystream.
-// Owner s writes chunk c at slot s*64 + (c ^ ((s>>1)&3))*16: conflict-free for
-// ds_write_b128's 8-lane groups; store lanes read linearly (conflict-free).
-__device__ __forceinline__ void crypt_message_staged(uint8_t *S, uint8_t *stage, Rc4Lane &st,
-                                                     uint8_t *msg, uint32_t len, uint4 (&A)[4],
-                                                     bool pre_in)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-#ifndef ZRC4_STAGGER
-#define ZRC4_STAGGER 0
-#endif
-#ifndef ZRC4_ABLATE
-#define ZRC4_ABLATE 0      // timing-only builds: 1 no stores, 2 no loads, 3 neither, 4 no staging/stores,
-                           // +8 no group-image load, +16 no group-image store (crypt_kernel)
-#endif
-    bool pre = pre_in;
-    uint32_t head = head_bytes(msg, len);
-    // Stagger (A/B knob): odd waves run half a block through the C step first,
-    // so their memory phases fall inside the even waves' keystream phases.
-    if (ZRC4_STAGGER && ((threadIdx.x >> 6) & 1u)) {
-        const uint32_t extra = len - head < 32u ? len - head : 32u;
-        head += extra;
-        pre = false;                      // the caller's preload started at offset 0
-    }
-    for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
-    msg += head;
-    len -= head;
-    uint4 *p = reinterpret_cast<uint4 *>(msg);
-    const uint32_t nblk = len >> 6;
-
-    // store-role addressing: session 16q + lane/4 of this wave, for q = 0..3
-    const uint32_t wmax = wave_max(nblk);
-    uint32_t snb[4];
-    gu8 *sbase[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int src = 16 * q + (int)(lane >> 2);
-        snb[q] = __shfl(nblk, src, 64);
-        const uint64_t b = __shfl((uint64_t)(uintptr_t)msg, src, 64);
-        const uint32_t c = (lane & 3u) ^ (((uint32_t)src >> 1) & 3u);
-        sbase[q] = reinterpret_cast<gu8 *>((uintptr_t)b) + c * 16u;
-    }
-    uint4 *wslot = reinterpret_cast<uint4 *>(stage + lane * 64u);
-    const uint32_t wsw = (lane >> 1) & 3u;
-    const uint4 *rslot = reinterpret_cast<const uint4 *>(stage + lane * 16u);
-
-    uint4 B[4];
-    if (!pre && nblk) load64(A, p);
-    auto block = [&](uint32_t blk, uint4(&cur)[4], uint4(&nxt)[4]) {
-        if (blk < nblk) {
-            if (!(ZRC4_ABLATE & 2)) load64(nxt, (blk + 1 < nblk) ? p + 4 * (blk + 1) : p + 4 * blk);
-            xor64_asm(st, cur);
-            if (ZRC4_ABLATE != 4) {
-#pragma unroll
-                for (int c = 0; c < 4; ++c) wslot[c ^ wsw] = cur[c];
-            }
-        }
-        if (ZRC4_ABLATE == 4) return;
-        // LDS ops of one wave execute in order; a compiler-only barrier keeps
-        // the staging reads below the other lanes' writes (no wait emitted).
-        asm volatile("" ::: "memory");
-        uint4 v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = rslot[q * 64];     // all reads, then stores
-        if (!(ZRC4_ABLATE & 1)) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (blk < snb[q])
-                    *reinterpret_cast<gu32x4 *>(sbase[q] + blk * 64u) = u32x4{v[q].x, v[q].y, v[q].z, v[q].w};
-        } else {
-            asm volatile("" :: "v"(v[0].x), "v"(v[1].x), "v"(v[2].x), "v"(v[3].x));
-        }
-        asm volatile("" ::: "memory");
-    };
-    for (uint32_t blk = 0; blk < wmax; blk += 2) {
-        block(blk, A, B);
-        if (blk + 1 >= wmax) break;
-        block(blk + 1, B, A);
-    }
-    p += 4 * nblk;
-    uint32_t rem = len & 63u;
-    while (rem >= 16u) {
-        *p = xor16(S, st, *p);
-        ++p;
-        rem -= 16u;
-    }
-    uint8_t *t = reinterpret_cast<uint8_t *>(p);
-    for (uint32_t i = 0; i < rem; ++i) t[i] ^= (uint8_t)prga_step(S, st);
-}
-
-__device__ __forceinline__ void load4(uint4 *q, const uint4 *p)
-{
-#pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = p[i];
-}
-
-__device__ __forceinline__ void xor64_asm_p(Rc4Lane &st, uint4 *q)
-{
-    xor64_asm(st, *reinterpret_cast<uint4(*)[4]>(q));
-}
-
-__device__ __forceinline__ void swap_halves(uint4 *lo, uint4 *hi)
-{
-    // v_permlane32_swap: lanes 32-63 of `lo` <-> lanes 0-31 of `hi`
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        auto rx = __builtin_amdgcn_permlane32_swap(lo[i].x, hi[i].x, false, false);
-        auto ry = __builtin_amdgcn_permlane32_swap(lo[i].y, hi[i].y, false, false);
-        auto rz = __builtin_amdgcn_permlane32_swap(lo[i].z, hi[i].z, false, false);
-        auto rw = __builtin_amdgcn_permlane32_swap(lo[i].w, hi[i].w, false, false);
-        lo[i] = make_uint4(rx[0], ry[0], rz[0], rw[0]);
-        hi[i] = make_uint4(rx[1], ry[1], rz[1], rw[1]);
-    }
-}
-
-// Staged message loop with WHOLE-LINE stores (the default staged path).
-//
-// Measured on gfx950 (tools/ubench/lds_ubench.hip, 8 waves/CU): stores where
-// 8 lanes write one full 128-B line run at 5.65 TB/s, 4-lane 64-B pieces at
-// 2.36 TB/s, per-lane 16-B pieces at 0.96 TB/s.  So results leave in whole
-// lines: a lane keeps two consecutive 64-B blocks (b, b+1) = one line of its
-// session, a v_permlane32_swap per dword hands block b+1 of the lower half to
-// the upper half and block b of the upper half to the lower half, and the
-// 4 KiB per-wave staging slot then holds 32 full lines per round (all 64 lanes
-// write 64 B each, two rounds per block pair).  Store lanes read the slot
-// linearly and write 8 sessions x 128 B per instruction.  The 16-B slot of
-// line chunk m of staging row r is (m + r) & 7: conflict-free ds_write_b128
-// for the 8-lane groups (distinct rows), conflict-free linear reads.
-// Loads stay per lane (5.5 TB/s), one block pair ahead.
-__device__ __forceinline__ void crypt_message_lines(uint8_t *S, uint8_t *stage, Rc4Lane &st,
-                                                    uint8_t *msg, uint32_t len, uint4 (&A)[4],
-                                                    bool pre)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t head = head_bytes(msg, len);
-    for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
-    msg += head;
-    len -= head;
-    uint4 *p = reinterpret_cast<uint4 *>(msg);
-    const uint32_t nblk = len >> 6;
-    const uint32_t last = nblk ? nblk - 1u : 0u;
-    const uint32_t wmax = wave_max(nblk);
-
-    // store role: round r, instruction q -> session 32r + 8q + lane/8, slot lane&7
-    uint32_t snb[2][4];
-    gu8 *sbase[2][4];
-    uint32_t smask[2][4];  // which line chunk this lane stores (byte offset m*16)
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int src = 32 * r + 8 * q + (int)(lane >> 3);
-            snb[r][q] = __shfl(nblk, src, 64);
-            const uint64_t b = __shfl((uint64_t)(uintptr_t)msg, src, 64);
-            const uint32_t row = (uint32_t)src & 31u;
-            const uint32_t m = ((lane & 7u) - row) & 7u;       // slot = (m + row) & 7
-            smask[r][q] = m;
-            sbase[r][q] = reinterpret_cast<gu8 *>((uintptr_t)b) + m * 16u;
-        }
-    // write role: row = lane & 31, half h = lane >> 5 (chunks 4h .. 4h+3)
-    const uint32_t wrow = lane & 31u, wh = lane >> 5;
-    uint8_t *wrow_base = stage + wrow * 128u;
-    const uint4 *rslot = reinterpret_cast<const uint4 *>(stage + lane * 16u);
-
-    auto stage_round = [&](int r, const uint4 *blk4, uint32_t b) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t m = 4u * wh + (uint32_t)c;
-            *reinterpret_cast<uint4 *>(wrow_base + (((m + wrow) & 7u) * 16u)) = blk4[c];
-        }
-        asm volatile("" ::: "memory");
-        uint4 v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = rslot[q * 64];
-        if (!(ZRC4_ABLATE & 1)) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                // chunk m lies in block b + (m >= 4) of the pair
-                if (b + (smask[r][q] >> 2) < snb[r][q])
-                    *reinterpret_cast<gu32x4 *>(sbase[r][q] + b * 64u) = u32x4{v[q].x, v[q].y, v[q].z, v[q].w};
-            }
-        } else {
-            asm volatile("" :: "v"(v[0].x), "v"(v[1].x), "v"(v[2].x), "v"(v[3].x));
-        }
-        asm volatile("" ::: "memory");
-    };
-
-    uint4 A1[4], B0[4], B1[4];
-    auto load_pair = [&](uint4 *d0, uint4 *d1, uint32_t b) {
-        if (ZRC4_ABLATE & 2) return;
-        const uint32_t b0 = b < last ? b : last, b1 = b + 1u < last ? b + 1u : last;
-        load4(d0, p + 4u * b0);
-        load4(d1, p + 4u * b1);
-    };
-    if (nblk && !(ZRC4_ABLATE & 2)) {
-        if (!pre) load4(A, p);
-        load4(A1, p + 4u * (1u < last ? 1u : last));
-    }
-    auto pair = [&](uint32_t b, uint4 *x0, uint4 *x1) {
-        if (b < nblk) xor64_asm_p(st, x0);
-        if (b + 1u < nblk) xor64_asm_p(st, x1);
-        if ((ZRC4_ABLATE & 4) == 0) {
-            swap_halves(x0, x1);
-            stage_round(0, x0, b);
-            stage_round(1, x1, b);
-        } else {
-            asm volatile("" :: "v"(x0[0].x), "v"(x1[0].x), "v"(x0[3].w), "v"(x1[3].w));
-        }
-    };
-    for (uint32_t b = 0; b < wmax; b += 4) {
-        if (nblk) load_pair(B0, B1, b + 2u);
-        pair(b, A, A1);
-        if (b + 2u >= wmax) break;
-        if (nblk) load_pair(A, A1, b + 4u);
-        pair(b + 2u, B0, B1);
-    }
-
-    p += 4u * nblk;
-    uint32_t rem = len & 63u;
-    while (rem >= 16u) {
-        *p = xor16(S, st, *p);
-        ++p;
-        rem -= 16u;
-    }
-    uint8_t *t = reinterpret_cast<uint8_t *>(p);
-    for (uint32_t i = 0; i < rem; ++i) t[i] ^= (uint8_t)prga_step(S, st);
-}
-
 // ---------------------------------------------------------------------------
-// Throughput-regime message loop with an in-register transpose (the default
-// store path when two workgroups share a CU).
+// Throughput-regime message loop with an in-register transpose (two
+// workgroups per CU, crypt_stream_kernel).
 //
-// Why: whole 128-byte lines are the only fast store shape (8 lanes per line:
-// 5.65 TB/s vs 0.96 TB/s for per-lane 16-B pieces, tools/ubench/lds_ubench.hip),
-// but a lane owns its own session's bytes.  crypt_message_lines gets there by
-// staging through LDS, which costs ~11 % extra LDS cycles in a kernel that is
-// LDS-bound at 8 waves/CU (ablation: profiles/r01_ab_ablation_v7.log).  Here
-// the 8x8 transpose of 16-byte chunks inside each group of 8 consecutive lanes
-// runs on VALU with v_cndmask_b32_dpp butterflies (96 VALU per line per lane,
-// no LDS), and the whole block loop is one asm statement generated by
-// tools/gen_line_loop.py (zrc4_line_loop.inc) so every VMEM op is issued with
-// the full exec mask and the vmcnt waits are exact static counts:
-//   * loads: the line two iterations ahead (blocks b+4, b+5), clamped to the
-//     lane's sink slot past its session's end;
-//   * stores: chunk i of the line of session 8g+q from lane 8g+i, or the sink
-//     past that session's last block (ragged batches);
+// Why: whole 128-byte lines are the only fast store shape at 8 waves/CU
+// (8 lanes per line: 5.65 TB/s vs 0.96 TB/s for per-lane 16-B pieces,
+// tools/ubench/lds_ubench.hip), but a lane owns its own session's bytes.
+// The 8x8 transpose of 16-byte chunks inside each group of 8 consecutive
+// lanes runs on VALU with v_cndmask_b32_dpp butterflies (96 VALU per line per
+// lane, no LDS: LDS staging cost ~11 % extra LDS cycles in this LDS-bound
+// regime, r01 ablation), and the whole block loop is one asm statement
+// generated by tools/gen_line_loop.py (zrc4_line_loop.inc) so every VMEM op
+// is issued with the full exec mask and the vmcnt waits are exact counts:
+//   * loads: per lane, the line two iterations ahead (blocks b+4, b+5),
+//     clamped to the lane's sink slot past its session's end (whole-line
+//     loads plus a second transpose were 4 % slower, r01);
+//   * stores (nt): chunk i of the line of session 8g+q from lane 8g+i, or the
+//     sink past that session's last block (ragged batches);
 //   * exec is narrowed only around the keystream of each 64-byte block.
 // The caller preloads lines 0 and 1 (P, Q) before the S-box image fill.
 // ---------------------------------------------------------------------------
@@ -836,14 +490,6 @@ __device__ __forceinline__ void preload_line(u32x32 &v, const uint8_t *b0, const
     }
 }
 
-// Loads stay per lane by default: whole-line loads (8 lanes per line, then a
-// second DPP transpose) measured 4 % slower on cfg5 (312.8 vs 300.2 us,
-// profiles/r01_ab_line_loads.log) -- per-lane 16-B loads already stream at
-// 5.5 TB/s and the extra 96 VALU per line cost more than they save.
-#ifndef ZRC4_LINE_LOADS
-#define ZRC4_LINE_LOADS 0    // 1: whole-line loads + a second transpose; 0: per-lane 16-B loads
-#endif
-
 // Everything about a group's messages the line loop needs that does not
 // depend on the S-boxes, so it can be computed (and the first two lines
 // loaded) before the group's S-box image is in LDS.
@@ -864,9 +510,9 @@ __device__ __forceinline__ void line_setup(LineSetup &ls, const uint8_t *msg, ui
     ls.wmax = __builtin_amdgcn_readfirstlane(wave_max(ls.nblk));
 }
 
-// Store (and, with line loads, load) role: lane 8g+i moves chunk i of the
-// line of session 8g+q at addr_q; lim_q = blocks of that session minus
-// (i >= 4), so chunk i of the line at block b exists iff b < lim_q.
+// Store role: lane 8g+i moves chunk i of the line of session 8g+q at addr_q;
+// lim_q = blocks of that session minus (i >= 4), so chunk i of the line at
+// block b exists iff b < lim_q.
 __device__ __forceinline__ void line_roles(u32x16 &addr, u32x8 &lim, const LineSetup &ls)
 {
     const uint32_t lane = threadIdx.x & 63u, i = lane & 7u;
@@ -881,33 +527,13 @@ __device__ __forceinline__ void line_roles(u32x16 &addr, u32x8 &lim, const LineS
     }
 }
 
-// Lines 0 and 1 in the layout the loop expects (sink past a session's end).
+// Lines 0 and 1 (the lane's own blocks 0..3; the sink past the session's end).
 __device__ __forceinline__ void preload_lines(u32x32 &P, u32x32 &Q, const LineSetup &ls, const uint8_t *sk)
 {
-#if ZRC4_LINE_LOADS
-    // tuple q = chunk i of the line of session 8g+q
-    u32x16 addr;
-    u32x8 lim;
-    line_roles(addr, lim, ls);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const uint8_t *a = reinterpret_cast<const uint8_t *>(
-            (uintptr_t)(((uint64_t)addr[2 * q + 1] << 32) | addr[2 * q]));
-        const u32x4 t0 = *reinterpret_cast<const u32x4 *>(lim[q] > 0u ? a : sk);
-        const u32x4 t1 = *reinterpret_cast<const u32x4 *>(lim[q] > 2u ? a + 128 : sk);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            P[4 * q + d] = t0[d];
-            Q[4 * q + d] = t1[d];
-        }
-    }
-#else
-    // the lane's own blocks 0..3
     const uint8_t *p = reinterpret_cast<const uint8_t *>((uintptr_t)ls.p);
     const uint32_t nb = ls.nblk;
     preload_line(P, nb > 0 ? p : sk, nb > 1 ? p + 64 : sk + 64);
     preload_line(Q, nb > 2 ? p + 128 : sk, nb > 3 ? p + 192 : sk + 64);
-#endif
 }
 
 __device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls,
@@ -923,13 +549,8 @@ __device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &
         "s_mov_b64 %[full], exec\n\t"
         "s_mov_b32 %[sb], 0\n\t"
         "LL_LOOP_%=:\n\t"
-#if ZRC4_LINE_LOADS
-        ZRC4_LC_HALF_P
-        ZRC4_LC_HALF_Q
-#else
         ZRC4_LL_HALF_P
         ZRC4_LL_HALF_Q
-#endif
         "s_branch LL_LOOP_%=\n\t"
         "LL_DONE_%=:\n\t"
         "s_mov_b64 exec, %[full]\n\t"
@@ -971,16 +592,6 @@ __device__ __forceinline__ void crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8
     for (uint32_t k = 0; k < rem; ++k) t[k] ^= (uint8_t)prga_step(S, st);
 }
 
-#ifndef ZRC4_STORE_PATH
-#define ZRC4_STORE_PATH 2    // staged launches: 0 quad stores via LDS, 1 line stores via LDS, 2 DPP transpose
-#endif
-
-// Which slot batch entry e maps to, and whether workgroup w owns one whole
-// aligned 256-slot group g (then state moves as a coalesced 64 KiB image).
-//   ids == NULL : slot = first_slot + e; whole iff first_slot % 256 == 0
-//                 (entries >= n of the last group belong to no other
-//                 workgroup; their state is copied back unchanged)
-//   ids != NULL : whole iff the 256 ids are exactly g*256 .. g*256+255
 #define ZRC4_INVALID 0xFFFFFFFFu
 
 // One group's 64 KiB S-box image, 16 x 16 B per lane into v160..v223, issued
@@ -1027,20 +638,31 @@ __device__ __forceinline__ void issue_image_asm(u32x32 &ilo, u32x32 &ihi, const 
 }
 
 // ---------------------------------------------------------------------------
-// crypt_kernel: batched RC4Encryption::encryption.
+// crypt_kernel: batched RC4Encryption::encryption, one group per workgroup
+// (launches with at most one group per CU: the chain-bound regime).
 // grid = ceil(n / 256) workgroups of 256 threads; workgroup w handles batch
-// entries [w*256, w*256+256).  The prologue issues every independent load
-// first (group image, len/off/xy, the first payload block) so it costs about
-// two HBM round trips instead of a dependent chain of them.
+// entries [w*256, w*256+256).  How entry e maps to a slot (MODE):
+//   kRange    slot = first_slot + e (ids == NULL; the bench's and the
+//             engine's contiguous batches).  The slot is arithmetic and the
+//             host has checked first_slot + n <= capacity, so the group image
+//             is issued from asm first, then len/off/x-y (no load waits on
+//             another: one HBM round trip); the first payload block is
+//             issued after a counted wait, so its round trip overlaps the LDS
+//             fill.  Whole (coalesced image) iff first_slot % 256 == 0.
+//   kGrouped  slot = ids[e]; the caller promises bucket w's non-idle entries
+//             all lie in ONE 256-slot group that no other bucket of the call
+//             touches (zrc4_crypt_grouped).  The group image moves as one
+//             coalesced copy and lane j runs in column col_of(slot & 255),
+//             so any subset of a group in any order costs what a whole group
+//             costs.  A bucket that mixes groups latches kErrGroup and is
+//             skipped.
+//   kIds      slot = ids[e], arbitrary: whole iff the 256 ids are exactly
+//             g*256 .. g*256+255 in order, otherwise each lane gathers and
+//             scatters its own 256-byte column (correct, strided).
 // ---------------------------------------------------------------------------
-//
-// RANGE (ids == NULL, the hook engine's and the bench's batches): the slot is
-// arithmetic and the host has checked first_slot + n <= capacity, so the
-// group image, len/off and x/y are issued together with no load waiting on
-// another (one HBM round trip instead of two); only the first payload block
-// waits for off/len.
-// ---------------------------------------------------------------------------
-template <bool STAGED, bool RANGE = false>
+enum CryptMode : int { kIds = 0, kRange = 1, kGrouped = 2 };
+
+template <int MODE>
 __global__ void __launch_bounds__(256, 2)
 crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
              const uint32_t *__restrict__ ids, uint32_t first_slot,
@@ -1048,19 +670,19 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
              const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
              uint32_t *__restrict__ err, uint8_t *__restrict__ sink)
 {
-    // one LDS object: 64 KiB S-box image (+ 4 x 4 KiB store staging for the
-    // LDS-staged store paths 0/1: 80 KiB, so two workgroups fill the CU's
-    // 160 KiB).  Path 2 (the default) runs throughput launches in
-    // crypt_stream_kernel instead.
-    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kSmemBytes : kGroupBytes + 16];
+    // one LDS object: the 64 KiB S-box image, then 16 B of workgroup flags
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kGroupBytes + 16];
     uint8_t *S = smem;
+    if (!lds_base_ok(S, err)) return;
+    Stamps ts;
+    stamp(ts, 0);
 
     const uint32_t j = threadIdx.x;
     const uint32_t e = blockIdx.x * kGroup + j;
     const bool valid = e < n;
     uint4 img[16];
     u32x32 ilo, ihi;
-    if constexpr (RANGE) {
+    if constexpr (MODE == kRange) {
         // Issued from asm, first: hipcc otherwise sinks these loads below its
         // wait for len/off.  Group (first_slot >> 8) + w lies inside the arena
         // even when first_slot is unaligned and the image goes unused.
@@ -1069,44 +691,67 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     const uint32_t mylen0 = valid ? len[e] : 0u;
     const uint64_t myoff = valid ? off[e] : 0u;
     uint32_t slot;
-    if constexpr (RANGE) {
+    if constexpr (MODE == kRange) {
         slot = valid ? first_slot + e : ZRC4_INVALID;
     } else {
-        slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
-        if (valid && slot >= capacity) {
-            latch_fault(err);
+        slot = valid ? ids[e] : ZRC4_INVALID;
+        // kGrouped pads buckets with ZRC4_IDLE_SLOT (0xFFFFFFFF) entries
+        if (valid && slot >= capacity && !(MODE == kGrouped && slot == ZRC4_INVALID)) {
+            latch_fault(err, kErrSlotRange);
             slot = ZRC4_INVALID;
         }
     }
     const bool active = slot != ZRC4_INVALID;
     const uint32_t mylen = active ? mylen0 : 0u;
-    const uint16_t sxy = (RANGE ? active : (active && mylen)) ? xy[slot] : (uint16_t)0;
+    const uint16_t sxy = (MODE == kRange ? active : (active && mylen)) ? xy[slot] : (uint16_t)0;
 
     bool whole;
     uint32_t g;
-    if (RANGE || !ids) {
+    uint32_t col = col_of(j);
+    volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(smem + kGroupBytes);
+    if constexpr (MODE == kRange) {
         whole = (first_slot & 255u) == 0u;
         g = (first_slot >> 8) + blockIdx.x;
+    } else if constexpr (MODE == kGrouped) {
+        // the bucket's group: min and max group of its busy entries must agree
+        if (j == 0) {
+            flag[0] = 0xFFFFFFFFu;
+            flag[1] = 0u;
+        }
+        __syncthreads();
+        const bool busy = active && mylen;
+        if (busy) {
+            atomicMin(const_cast<uint32_t *>(flag), slot >> 8);
+            atomicMax(const_cast<uint32_t *>(flag + 1), slot >> 8);
+        }
+        __syncthreads();
+        const uint32_t gmin = flag[0], gmax = flag[1];
+        __syncthreads();
+        if (gmin == 0xFFFFFFFFu) return;                  // an idle bucket
+        if (gmin != gmax) {
+            if (j == 0) latch_fault(err, kErrGroup);
+            return;
+        }
+        whole = true;
+        g = gmin;
+        col = col_of(slot & 255u);
     } else {
         const uint32_t first = ids[blockIdx.x * kGroup];
         g = first >> 8;
-        // workgroup AND through one staging word (no extra LDS allocation)
-        volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(smem + kGroupBytes);
-        if (j == 0) *flag = 1u;
+        if (j == 0) flag[0] = 1u;
         __syncthreads();
-        if (!(active && slot == ((first & ~255u) + j) && (first & 255u) == 0u)) *flag = 0u;
+        if (!(active && slot == ((first & ~255u) + j) && (first & 255u) == 0u)) flag[0] = 0u;
         __syncthreads();
-        whole = *flag != 0u;
+        whole = flag[0] != 0u;
         __syncthreads();
     }
 
-    const uint32_t col = col_of(j);
     uint8_t *msg = payload + myoff;
     uint4 A[4];
     const bool pre = active && mylen >= 64u && head_bytes(msg, mylen) == 0u;
-    if constexpr (RANGE) {
-        // The image was issued before len, off and x/y (3 loads).  Waited
-        // on every path (the registers must not be reused while it is in
+    if constexpr (MODE == kRange) {
+        // The image was issued before len, off and x/y (3 loads).  Waited on
+        // every path (the registers must not be reused while it is in
         // flight); the first payload block is issued after this wait, so its
         // round trip overlaps the LDS fill.
         asm volatile("s_waitcnt vmcnt(3)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
@@ -1117,8 +762,7 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         }
     }
     if (whole) {
-        if (!(ZRC4_ABLATE & 8)) {
-        if constexpr (!RANGE) {
+        if constexpr (MODE != kRange) {
             const uint4 *src = reinterpret_cast<const uint4 *>(arena + (size_t)g * kGroupBytes);
 #pragma unroll
             for (int i = 0; i < 16; ++i) img[i] = src[i * 256 + j];
@@ -1127,59 +771,32 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         uint4 *dst = reinterpret_cast<uint4 *>(S);
 #pragma unroll
         for (int i = 0; i < 16; ++i) dst[i * 256 + j] = img[i];
-        } else if (pre) {
-            issue_block_asm(A, msg);
-        }
         __syncthreads();
     } else {
         if (pre) issue_block_asm(A, msg);
         if (active && mylen) gather_column(S, col, arena, slot);
     }
+    stamp(ts, 1);
 
-    if (STAGED) {
-    // Every lane of a wave takes part in the staged stores, so the message
-    // loop runs for all lanes (an idle lane has len 0: no keystream, no state
-    // change) and only the state write-back is predicated.
-    {
-        const uint32_t x = sxy & 255u, y = sxy >> 8;
+    if (active && mylen) {
         Rc4Lane st;
-        st.col = col;
-        st.x0 = (((x + 1u) & 255u) << 8) | col;
-        st.a0 = S[st.x0];
-        st.ya = (y << 8) | col;
-        st.ta = col;
-        st.x1 = col;
-        if constexpr (ZRC4_STORE_PATH == 1)
-            crypt_message_lines(S, smem + kGroupBytes + (j >> 6) * kStageBytes, st, msg, mylen, A, pre);
-        else
-            crypt_message_staged(S, smem + kGroupBytes + (j >> 6) * kStageBytes, st, msg, mylen, A, pre);
-        if (active && mylen)
-            xy[slot] = (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
-    }
-    } else if (active && mylen) {
-        const uint32_t x = sxy & 255u, y = sxy >> 8;
-        Rc4Lane st;
-        st.col = col;
-        st.x0 = (((x + 1u) & 255u) << 8) | col;
-        st.a0 = S[st.x0];
-        st.ya = (y << 8) | col;
-        st.ta = col;
-        st.x1 = col;
+        lane_init(st, S, col, sxy);
         crypt_message(S, st, msg, mylen, A, pre);
-        xy[slot] = (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
+        xy[slot] = lane_xy(st);
     }
+    stamp(ts, 2);
 
     if (whole) {
         __syncthreads();
-        if (ZRC4_ABLATE & 16) {
-        } else if (ZRC4_DIRECT_IMG_NT) {
-            lds_to_image_nt(arena + (size_t)g * kGroupBytes, S);
-        } else {
-            lds_to_image(arena + (size_t)g * kGroupBytes, S);
-        }
+        lds_to_image(arena + (size_t)g * kGroupBytes, S);
     } else if (active && mylen) {
         scatter_column(arena, slot, S, col);
     }
+#if ZRC4_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    stamp(ts, 3);
+    stamps_out(ts, sink);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1189,16 +806,17 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 // With one group per workgroup every workgroup of a round loads its 64 KiB
 // S-box image, runs, and stores the image at the same time, so the HBM idles
 // during the keystream and the LDS idles during the image bursts (the
-// ablation put the image I/O at 42 us of a 330 us cfg5 launch,
-// profiles/r01_ab_ablation_v7.log).  Here grid = 2 workgroups per CU and each
-// workgroup walks groups w, w + grid, ...; while group w's keystream runs, the
-// next group's image (16 x 16 B per lane, in VGPRs), its batch entries and --
-// once the message loop is done -- its first two payload lines are already in
-// flight, and the finished image goes back to HBM behind the next group's
-// work.  At a boundary only the LDS copies and three barriers remain.
+// ablation put the image I/O at 42 us of a 330 us cfg5 launch, r01).  Here
+// grid = 2 workgroups per CU and each workgroup walks groups w, w + grid, ...;
+// while group w's keystream runs, the next group's image (16 x 16 B per lane,
+// in VGPRs), its batch entries and -- once the message loop is done -- its
+// first two payload lines are already in flight, and the finished image goes
+// back to HBM behind the next group's work.  At a boundary only the LDS
+// copies and three barriers remain.
 //   PF = range batch with first_slot % 256 == 0: every group is a whole,
 //        aligned image and is prefetched; otherwise (ids, unaligned range)
-//        each group decides whole/gather as crypt_kernel does, unprefetched.
+//        each group decides whole/gather as crypt_kernel<kIds> does,
+//        unprefetched.
 // ---------------------------------------------------------------------------
 struct EntryIn {
     uint32_t len;    // 0 for idle lanes
@@ -1215,7 +833,7 @@ __device__ __forceinline__ void load_entry(EntryIn &d, uint32_t w, const uint32_
     const bool valid = e < n;
     uint32_t slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
     if (valid && slot >= capacity) {
-        latch_fault(err);
+        latch_fault(err, kErrSlotRange);
         slot = ZRC4_INVALID;
     }
     // No load here depends on another's value (the range path's slot is
@@ -1225,7 +843,6 @@ __device__ __forceinline__ void load_entry(EntryIn &d, uint32_t w, const uint32_
     d.slot = slot;
     d.xy = (slot != ZRC4_INVALID) ? xy[slot] : 0u;
 }
-
 
 // Next group's batch entries and S-box image, issued from asm so the compiler
 // neither waits for them nor counts them: it would otherwise drain them at
@@ -1293,6 +910,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kGroupBytes + 16];
     uint8_t *S = smem;
+    if (!lds_base_ok(S, err)) return;
     const uint32_t j = threadIdx.x;
     const uint32_t col = col_of(j);
     const uint32_t nwg = (n + kGroup - 1) / kGroup;
@@ -1346,9 +964,16 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                 whole = (first_slot & 255u) == 0u;
                 g = (first_slot >> 8) + w;
             } else {
+                // workgroup AND through a flag word after the image (LDS offset
+                // 0 stays the S-box image)
                 const uint32_t first = ids[w * kGroup];
                 g = first >> 8;
-                whole = __syncthreads_and(active && cur.slot == ((first & ~255u) + j) && (first & 255u) == 0u);
+                volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(smem + kGroupBytes);
+                if (j == 0) flag[0] = 1u;
+                __syncthreads();
+                if (!(active && cur.slot == ((first & ~255u) + j) && (first & 255u) == 0u)) flag[0] = 0u;
+                __syncthreads();
+                whole = flag[0] != 0u;
             }
             if (whole) {
                 image_to_lds(S, arena + (size_t)g * kGroupBytes);
@@ -1379,17 +1004,10 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 
         // ---- keystream over this group's messages
         {
-            const uint32_t x = cur.xy & 255u, y = (cur.xy >> 8) & 255u;
             Rc4Lane st;
-            st.col = col;
-            st.x0 = (((x + 1u) & 255u) << 8) | col;
-            st.a0 = S[st.x0];
-            st.ya = (y << 8) | col;
-            st.ta = col;
-            st.x1 = col;
+            lane_init(st, S, col, cur.xy);
             crypt_message_dpp(S, st, payload + cur.off, cur.len, P, Q, ls, sk);
-            if (active && cur.len)
-                xy[cur.slot] = (uint16_t)((((st.x0 >> 8) - 1u) & 255u) | (st.ya & 0xFF00u));
+            if (active && cur.len) xy[cur.slot] = lane_xy(st);
         }
 
         EntryIn nxt = {0u, ZRC4_INVALID, 0u, 0u};
@@ -1412,10 +1030,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         // ---- this group's state back to HBM
         if (whole) {
             __syncthreads();
-            if (ZRC4_IMG_NT)
-                lds_to_image_nt(arena + (size_t)g * kGroupBytes, S);
-            else
-                lds_to_image(arena + (size_t)g * kGroupBytes, S);
+            lds_to_image(arena + (size_t)g * kGroupBytes, S);
         } else if (active && cur.len) {
             scatter_column(arena, cur.slot, S, col);
         }
@@ -1439,7 +1054,11 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 // 3 VALU + 4 LDS + 2 waits; S[i+1] is read after the S[j] = a write, so no
 // forwarding is needed (S[i] = b goes to i != i+1).  Writing S[j] before S[i]
 // swaps the reference's order (:63-64); they only collide when i == j, and
-// then b == a.  Key bytes for 16 steps are fetched one chunk ahead.
+// then b == a.
+// Key schedule: key lengths dividing 16 keep a 16-byte pattern in 4 VGPRs,
+// 32- and 64-byte keys a 64-byte pattern in 16 VGPRs (step u adds pattern
+// byte (u+1) mod the chunk length through the SDWA source selector, no key
+// loads in the loop); other lengths fetch 16 key bytes one chunk ahead.
 // ---------------------------------------------------------------------------
 #define ZRC4_KSA_STEP_SEL(XC, XN, A, P, KN, SEL)                                                 \
     "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
@@ -1457,8 +1076,6 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #define ZRC4_KSA_STEP(XC, XN, A, P, KN) ZRC4_KSA_STEP_SEL(XC, XN, A, P, KN, BYTE_0)
 #define ZRC4_KSA_PAIR(K1, K2)                                                                    \
     ZRC4_KSA_STEP(x0, x1, a0, a1, K1) ZRC4_KSA_STEP(x1, x0, a1, a0, K2)
-// Key pattern in registers (byte u of q = key[u % len]): step u of a 16- or
-// 64-step chunk adds pattern byte (u + 1) mod the chunk length.
 #define ZRC4_KSA_QPAIR(K1, S1, K2, S2)                                                           \
     ZRC4_KSA_STEP_SEL(x0, x1, a0, a1, K1, S1) ZRC4_KSA_STEP_SEL(x1, x0, a1, a0, K2, S2)
 
@@ -1519,13 +1136,6 @@ __device__ __forceinline__ void ksa64_pattern_asm(uint32_t &x0, uint32_t &x1, ui
         : "memory");
 }
 
-#ifndef ZRC4_KSA_ASM
-#define ZRC4_KSA_ASM 1      // 0: the portable C step (A/B builds)
-#endif
-#ifndef ZRC4_KSA_PATTERN
-#define ZRC4_KSA_PATTERN 1  // key lengths 1-16 (dividing 16), 32 and 64 keep the key schedule in registers (0: A/B builds)
-#endif
-
 __global__ void __launch_bounds__(256, 2)
 ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
            const uint32_t *__restrict__ ids, uint32_t first_slot,
@@ -1533,14 +1143,16 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
            const uint64_t *__restrict__ key_off, const uint32_t *__restrict__ key_len,
            uint32_t n, uint32_t capacity, uint32_t *__restrict__ err)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t S[kGroupBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kGroupBytes + 16];
+    uint8_t *S = smem;
+    if (!lds_base_ok(S, err)) return;
 
     const uint32_t j = threadIdx.x;
     const uint32_t e = blockIdx.x * kGroup + j;
     const bool valid = e < n;
     uint32_t slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
     if (valid && slot >= capacity) {
-        latch_fault(err);
+        latch_fault(err, kErrSlotRange);
         slot = ZRC4_INVALID;
     }
     const bool active = slot != ZRC4_INVALID;
@@ -1557,7 +1169,13 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     } else {
         const uint32_t first = (blockIdx.x * kGroup < n) ? ids[blockIdx.x * kGroup] : 0u;
         g = first >> 8;
-        whole = __syncthreads_and(active && slot == ((first & ~255u) + j) && (first & 255u) == 0u);
+        volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(smem + kGroupBytes);
+        if (j == 0) flag[0] = 1u;
+        __syncthreads();
+        if (!(active && slot == ((first & ~255u) + j) && (first & 255u) == 0u)) flag[0] = 0u;
+        __syncthreads();
+        whole = flag[0] != 0u;
+        __syncthreads();
     }
     const bool partial = (blockIdx.x + 1u) * kGroup > n;
     const uint32_t col = col_of(j);
@@ -1584,8 +1202,7 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     }
 
     if (active && kl) {
-        constexpr bool kPattern = (ZRC4_KSA_ASM != 0) && (ZRC4_KSA_PATTERN != 0);
-        if (kPattern && kl <= 16u && (16u % kl) == 0u) {
+        if (kl <= 16u && (16u % kl) == 0u) {
             // the whole key schedule (:67-70) in 16 register bytes, loaded once
             uint32_t q[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -1593,7 +1210,7 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col];
             uint32_t ya = col | ((q[0] & 0xFFu) << 8);    // j = 0 + key[0] before step 0
             for (int c = 0; c < 16; ++c) ksa16_pattern_asm(x0, x1, a0, ya, q);
-        } else if (kPattern && (kl == 32u || kl == 64u)) {
+        } else if (kl == 32u || kl == 64u) {
             // 32- and 64-byte keys: the schedule in 64 register bytes
             uint32_t q[16];
 #pragma unroll
@@ -1603,7 +1220,7 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col];
             uint32_t ya = col | ((q[0] & 0xFFu) << 8);
             for (int c = 0; c < 4; ++c) ksa64_pattern_asm(x0, x1, a0, ya, q);
-        } else if (ZRC4_KSA_ASM) {
+        } else {
             // key bytes of steps 16c .. 16c+16, fetched one chunk ahead
             uint32_t kk = 0;
             auto fetch = [&](uint32_t (&kb)[17]) {
@@ -1627,25 +1244,6 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #pragma unroll
                 for (int u = 0; u < 17; ++u) cur[u] = nxt[u];
             }
-        } else {
-            uint32_t jj = 0, kk = 0;
-            for (int i0 = 0; i0 < 256; i0 += 16) {
-                uint32_t kb[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {      // key[k], k cycles mod len (:67-70)
-                    kb[u] = key[kk];
-                    if (++kk >= kl) kk = 0;
-                }
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const uint32_t ia = ((uint32_t)(i0 + u) << 8) | col;
-                    const uint32_t v = S[ia];
-                    jj = (jj + v + kb[u]) & 255u;   // j = (u8)(j + tmp + obs[k])
-                    const uint32_t ja = (jj << 8) | col;
-                    S[ia] = S[ja];
-                    S[ja] = (uint8_t)v;
-                }
-            }
         }
     }
     if (active) xy[slot] = 0;                        // _x = _y = 0 (:48-49)
@@ -1659,13 +1257,12 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 
 // ---------------------------------------------------------------------------
 // xor_ring_kernel: payload spans XOR pre-generated keystream from per-slot
-// device rings (the session engine's latency path, zrc4_xor_ring).
-// One workgroup per entry.  Payload is walked in dwords aligned to its own
-// address (whole dwords: one 4-byte RMW; the two edge dwords: byte RMWs, so no
-// byte outside the span is ever written); the ring is read bytewise at
-// (pos + i) mod cap and the bytes used are zeroed, so the next zrc4_crypt
-// over them (0 ^ k = k) refills pure keystream.  Consecutive lanes touch
-// consecutive dwords / ring bytes (coalesced).
+// device rings (zrc4_xor_ring).  One workgroup per entry.  Payload is walked
+// in dwords aligned to its own address (whole dwords: one 4-byte RMW; the two
+// edge dwords: byte RMWs, so no byte outside the span is ever written); the
+// ring is read bytewise at (pos + i) mod cap and the bytes used are zeroed,
+// so the next zrc4_crypt over them (0 ^ k = k) refills pure keystream.
+// Consecutive lanes touch consecutive dwords / ring bytes (coalesced).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
 xor_ring_kernel(uint8_t *__restrict__ ring, uint32_t cap, const uint32_t *__restrict__ rid,
