@@ -293,7 +293,7 @@ def kernel_name(S: int) -> str:
     except Exception:
         cus = 256
     groups = -(-S // 256)
-    return "zrc4::crypt_stream_kernel<true>" if groups > cus else "zrc4::crypt_kernel<false, true>"
+    return "zrc4::crypt_stream_kernel<true>" if groups > cus else "zrc4::crypt_kernel<1, false>"
 
 
 def load_traffic(workload: str):
@@ -309,10 +309,28 @@ def load_traffic(workload: str):
 
 
 # ------------------------------------------------------------- CPU baseline
+def cgroup_cpu_quota():
+    """The container's CPU quota (cgroup v2 cpu.max / v1 cfs), or None."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        return None if q <= 0 else round(q / per, 2)
+    except Exception:
+        return None
+
+
 def cpu_baseline(args, S, L):
     """The oracle restatement (a -O3 C port of rc4_encryption.h:74-93) timed on
     this host on a bounded sample of the same workload (same keys, payload and
-    pre-advance as rank 0's first batch).  Reported, not optimised against."""
+    pre-advance as rank 0's first batch): 1 thread (the reference's single
+    event-loop thread), then one worker per core in this process's affinity
+    mask, each re-crypting its round-robin share for the whole window (one
+    thread start per worker).  Reported, not optimised against."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle  # cpu_baseline leg only
     from zsummerx_amd import synth
@@ -321,36 +339,26 @@ def cpu_baseline(args, S, L):
         cores = len(os.sched_getaffinity(0))
     except Exception:
         cores = os.cpu_count() or 1
-    cores = max(1, min(cores, args.cpu_threads))
+    if args.cpu_threads > 0:
+        cores = min(cores, args.cpu_threads)
     w = synth.make(0, S, L, threads=8)
     ob = pyoracle.Batch(S)
     ob.make_sbox(w.keys, w.key_off, w.key_len)
     ob.crypt(np.zeros(1000, dtype=np.uint8), np.zeros(S, dtype=np.uint64), w.adv)
-    budget = args.cpu_seconds
+    pay = w.payload.copy()
+    reps = 5
+    win = args.cpu_seconds / 2 / reps
 
-    def timed(threads, secs):
-        pay = w.payload.copy()
-        runs = []
-        t_end = time.perf_counter() + secs
-        while len(runs) < 5 or time.perf_counter() < t_end:
-            reps, t0 = 0, time.perf_counter()
-            while True:
-                ob.crypt(pay, w.off, w.length, threads=threads)
-                reps += 1
-                dt = time.perf_counter() - t0
-                if dt >= 0.2:
-                    break
-            runs.append(reps * S * L / dt / GIB)
-            if len(runs) >= 50:
-                break
-        return statistics.median(runs)
+    def rate(threads):
+        return statistics.median(ob.crypt_rate(pay, w.off, w.length, threads, win) for _ in range(reps)) / GIB
 
-    one = timed(1, budget / 2)
-    many = timed(cores, budget / 2) if cores > 1 else one
+    one = rate(1)
+    many = rate(cores) if cores > 1 else one
     return {"value": round(many, 4), "unit": "GiB/s", "cores": cores, "kind": "port",
-            "value_1thread": round(one, 4),
-            "sample": f"{args.workload} batch ({S} x {L} B) re-crypted repeatedly, "
-                      f"~{budget:.0f}s total: median of >=5 runs of >=200 ms, 1 thread then {cores} threads"}
+            "value_1thread": round(one, 4), "hardware_concurrency": os.cpu_count(),
+            "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "sample": f"{args.workload} batch ({S} x {L} B) re-crypted for {win:.1f} s windows, median of {reps}: "
+                      f"1 thread, then {cores} threads (every core in the affinity mask)"}
 
 
 # ------------------------------------------------------- host-inclusive rate
@@ -552,12 +560,33 @@ def frame_bench(args):
         scratch = T(np.zeros(S * L, dtype=np.uint8))
         t_crypt = timed(lambda: ctx.crypt_range(0, scratch, d_off, d_len, n=S, stream=st))
         ctx.sync(st)
+        # Decrypt + frame: each session's block = [L bytes of packets | L-byte
+        # fresh tail]; the tail is decrypted, the packet part framed (kept out
+        # of the decrypt so repeated launches frame the same packets).  Fused
+        # (zrc4_crypt_range_frame: one launch) vs two launches.
+        blk = np.zeros(S * 2 * L, dtype=np.uint8)
+        blk.reshape(S, 2 * L)[:, :L] = buf.reshape(S, L)
+        d_blk = T(blk)
+        f_off = T((np.arange(S, dtype=np.int64) * 2 * L))
+        t_off = T((np.arange(S, dtype=np.int64) * 2 * L + L))
+        frame = {"off": f_off, "len": d_len, "bound": bound, "npk": npk, "used": used, "status": status}
+        t_fused = timed(lambda: ctx.crypt_range_frame(0, d_blk, t_off, d_len, frame, n=S, stream=st))
+        ctx.sync(st)
+        fused_npk = int(npk.sum().item())
+
+        def two_launches():
+            ctx.crypt_range(0, d_blk, t_off, d_len, n=S, stream=st)
+            ctx.frame_scan(d_blk, f_off, d_len, bound, npk, used, status, stream=st)
+        t_two = timed(two_launches)
+        ctx.sync(st)
     out = {"metric": "proto4z frame scan (device-resident, decrypted buffers)", "workload": args.workload,
            "sessions": S, "bytes_per_session": L, "packets_per_launch": got_npk,
            "packets_expected": npk_total, "kernel_us": round(t_scan * 1e6, 3),
            "framed_gib_s": round(S * L / t_scan / GIB, 2), "packets_per_s": round(got_npk / t_scan, 1),
            "crypt_kernel_us_same_batch": round(t_crypt * 1e6, 3),
            "scan_share_of_decrypt_plus_scan": round(t_scan / (t_scan + t_crypt), 4),
+           "fused_decrypt_frame_us": round(t_fused * 1e6, 3), "two_launches_us": round(t_two * 1e6, 3),
+           "fused_saves_us": round((t_two - t_fused) * 1e6, 3),
            "note": "scan reads 4 header bytes per packet; latency-bound chain of header reads per session"}
     if args.cpu_seconds > 0:
         sys.path.insert(0, str(ROOT / "oracle"))
@@ -576,6 +605,7 @@ def frame_bench(args):
                                "kind": "port", "sample": f"the same {S} buffers, oracle_frame_scan, median of {len(runs)}"}
         out["speedup_vs_1_core"] = round(cpu / t_scan, 1)
     assert got_npk == npk_total, (got_npk, npk_total)
+    assert fused_npk == npk_total, (fused_npk, npk_total)
     return out
 
 
@@ -591,7 +621,8 @@ def parse(argv=None):
                    help="rotate over distinct batches totalling this many MiB per GPU (0 = one batch)")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="CPU baseline time budget on rank 0 at N=1 (0 disables)")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="cap on CPU-baseline threads (0 = every core in the affinity mask)")
     p.add_argument("--event-every", type=int, default=16,
                    help="launches per HIP-event segment (kernel duration = segment time / N)")
     p.add_argument("--host-inclusive", action="store_true",

@@ -167,6 +167,33 @@ int zrc4_frame_scan(zrc4_ctx *ctx, const uint8_t *buf, const uint64_t *off,
                     uint32_t max_packets, uint32_t *npk, uint32_t *used,
                     uint32_t *status, uint32_t *pkt_len, void *stream);
 
+/* Decrypt + frame in ONE launch (the recv hook followed by onRecv's framing
+ * loop, src/frame/session.cpp:313-371): zrc4_crypt_range / zrc4_crypt_grouped
+ * semantics for the crypt, then for every entry i the zrc4_frame_scan walk of
+ * payload[frame->off[i] .. frame->off[i] + frame->len[i]) (the whole receive
+ * block, which may start before the decrypted tail) into npk/used/status/
+ * pkt_len[i] exactly as zrc4_frame_scan defines them.  In the chain-bound
+ * regime (at most one slot group per CU) each lane frames its own session in
+ * the crypt kernel's epilogue; larger batches run the throughput kernel and
+ * the scan as a second launch.  Outputs of a bucket refused with
+ * ZRC4_ERR_GROUP are unspecified.  Device pointers; asynchronous. */
+typedef struct zrc4_frame_args {
+    const uint64_t *off;
+    const uint32_t *len;
+    uint32_t bound;
+    uint32_t max_packets;
+    uint32_t *npk;
+    uint32_t *used;
+    uint32_t *status;
+    uint32_t *pkt_len;
+} zrc4_frame_args;
+int zrc4_crypt_range_frame(zrc4_ctx *ctx, uint32_t first_slot, uint8_t *payload,
+                           const uint64_t *off, const uint32_t *len, uint32_t n,
+                           const zrc4_frame_args *frame, void *stream);
+int zrc4_crypt_grouped_frame(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payload,
+                             const uint64_t *off, const uint32_t *len, uint32_t n,
+                             const zrc4_frame_args *frame, void *stream);
+
 /* Wait for `stream`, then report (and clear) any latched device-side fault. */
 int zrc4_sync(zrc4_ctx *ctx, void *stream);
 

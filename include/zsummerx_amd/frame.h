@@ -80,6 +80,7 @@ enum StatType {
     STAT_RC4_SPANS,      // spans crypted (reference: one encryption() call each)
     STAT_RC4_BYTES,      // bytes crypted
     STAT_RC4_NANOS,      // wall time inside Rc4Hooks::crypt
+    STAT_RC4_FRAMED,     // receive blocks framed on the device (setDeviceFraming)
     STAT_SIZE,
 };
 
@@ -200,6 +201,11 @@ public:
     // 2 * maxSessions) the first time a session with a key needs one).
     void setRc4Hooks(std::unique_ptr<Rc4Hooks> hooks);
     Rc4Hooks *rc4Hooks() const { return _rc4.get(); }
+    // Frame decrypted receive blocks on the device, fused into the decrypt
+    // launch (Rc4Hooks::cryptFrame), for sessions whose
+    // _onRawPacketCheck is the default proto4z check.  Needs hooks with
+    // canFrame() (the direct device hooks); otherwise framing stays on the host.
+    void setDeviceFraming(bool on) { _deviceFraming = on; }
 
     bool start();
     void stop();
@@ -248,7 +254,7 @@ private:
     void markDirty(TcpSession &s);
     void writeSending(const TcpSessionPtr &s);
     void setWantOut(TcpSession &s, bool on);
-    void dispatchRecv(const TcpSessionPtr &s);
+    void dispatchRecv(const TcpSessionPtr &s, const Rc4Frame *fr = nullptr);
     void flushHooks();
     void finishCloses();
 
@@ -270,6 +276,9 @@ private:
     std::vector<TcpSessionPtr> _sendBatch;    // sessions whose _sending is in this crypt
     std::vector<TcpSessionPtr> _closeList;
     std::vector<Rc4Span> _spans;
+    std::vector<Rc4Frame> _frames;            // parallel to _spans when framing on the device
+    std::vector<int> _recvFrame;              // _recvBatch[i] -> its frame in _frames, or -1
+    bool _deviceFraming = false;
     std::vector<std::function<void()>> _posted;
 
     // slots and blocks

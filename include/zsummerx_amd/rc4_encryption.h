@@ -11,13 +11,16 @@
 // (the reference session would have crashed on garbage instead; see
 // INTEGRATION.md for the batched, error-returning path the hooks should use).
 //
-// Each RC4Encryption owns one slot (stream) of a process-wide device arena.
-// A TcpSession owns two (_rc4StateRead/_rc4StateWrite, session.h:115-116).
-// The per-call path copies host<->device, so it is a correctness drop-in; the
-// throughput path is Rc4Batch (one launch per event-loop iteration).
+// Each RC4Encryption owns one slot (stream) of a process-wide device arena
+// that grows in 65 536-stream chunks.  A TcpSession owns two
+// (_rc4StateRead/_rc4StateWrite, session.h:115-116).  The per-call path runs
+// the kernel on a pinned staging copy of the caller's bytes (one launch and
+// one wait per call), so it is a correctness drop-in; the throughput path is
+// Rc4Batch or the batched engine (one launch per event-loop iteration).
 #pragma once
 
 #include <cstdint>
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -33,60 +36,103 @@ inline void zrc4_throw(int rc, const char *what)
         throw std::runtime_error(std::string(what) + ": " + zrc4_strerror(rc));
 }
 
-// Process-wide arena with a free list of slots.
+// Process-wide arena: device contexts of kChunk streams each, created on
+// demand (a 100K-connection server needs 200K streams; each chunk is a 16 MiB
+// S-box arena), with a free list of slots.  Slot id = chunk * kChunk + local.
+// Device: $ZSX_RC4_DEVICE (default 0).  Thread-safe.
 class Rc4Arena {
 public:
-    static Rc4Arena &instance(uint32_t capacity = 1u << 17, int device = 0)
+    static constexpr uint32_t kChunk = 1u << 16;
+
+    static Rc4Arena &instance()
     {
-        static Rc4Arena a(capacity, device);
+        static Rc4Arena a;
         return a;
     }
-    zrc4_ctx *ctx() const { return ctx_; }
+    zrc4_ctx *ctx(uint32_t slot)
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        return chunks_[slot / kChunk];
+    }
+    static uint32_t local(uint32_t slot) { return slot % kChunk; }
+
     uint32_t acquire()
     {
         std::lock_guard<std::mutex> g(mu_);
         if (!free_.empty()) {
-            uint32_t s = free_.back();
+            const uint32_t s = free_.back();
             free_.pop_back();
             return s;
         }
-        if (next_ >= zrc4_capacity(ctx_)) throw std::runtime_error("zrc4 arena out of slots");
-        return next_++;
+        if (next_ == (uint64_t)chunks_.size() * kChunk) {
+            zrc4_ctx *c = nullptr;
+            zrc4_throw(zrc4_create(&c, device_, kChunk), "zrc4_create");
+            chunks_.push_back(c);
+        }
+        return (uint32_t)next_++;
     }
+    // The slot goes back to the empty-key state (identity box, x = y = 0:
+    // makeSBox(""), rc4_encryption.h:48-56) so its next owner never sees the
+    // previous stream.
     void release(uint32_t s)
     {
+        zrc4_ctx *c = ctx(s);
+        uint8_t id[256];
+        for (int i = 0; i < 256; ++i) id[i] = (uint8_t)i;
+        const int rc = zrc4_set_state(c, local(s), id, 0, 0);
         std::lock_guard<std::mutex> g(mu_);
-        free_.push_back(s);
+        if (rc == ZRC4_OK) free_.push_back(s);   // a slot that cannot be reset is not reused
     }
     ~Rc4Arena()
     {
-        if (ctx_) zrc4_destroy(ctx_);
+        for (zrc4_ctx *c : chunks_) zrc4_destroy(c);
     }
 
 private:
-    Rc4Arena(uint32_t capacity, int device)
+    Rc4Arena()
     {
-        zrc4_throw(zrc4_create(&ctx_, device, capacity), "zrc4_create");
+        const char *d = std::getenv("ZSX_RC4_DEVICE");
+        device_ = d ? std::atoi(d) : 0;
     }
-    zrc4_ctx *ctx_ = nullptr;
+    int device_ = 0;
     std::mutex mu_;
+    std::vector<zrc4_ctx *> chunks_;
     std::vector<uint32_t> free_;
-    uint32_t next_ = 0;
+    uint64_t next_ = 0;
 };
 
 class RC4Encryption {
 public:
     RC4Encryption() : slot_(Rc4Arena::instance().acquire()) {}
-    ~RC4Encryption() { Rc4Arena::instance().release(slot_); }
-    RC4Encryption(const RC4Encryption &) = delete;
-    RC4Encryption &operator=(const RC4Encryption &) = delete;
+    ~RC4Encryption()
+    {
+        if (slot_ != kNoSlot) Rc4Arena::instance().release(slot_);
+    }
+    // A value type like the reference (an int[256] + x + y member block): a
+    // copy owns its own slot holding the same state.
+    RC4Encryption(const RC4Encryption &o) : slot_(Rc4Arena::instance().acquire()) { copyState(o); }
+    RC4Encryption &operator=(const RC4Encryption &o)
+    {
+        if (this != &o) copyState(o);
+        return *this;
+    }
+    RC4Encryption(RC4Encryption &&o) noexcept : slot_(o.slot_) { o.slot_ = kNoSlot; }
+    RC4Encryption &operator=(RC4Encryption &&o) noexcept
+    {
+        if (this != &o) {
+            if (slot_ != kNoSlot) Rc4Arena::instance().release(slot_);
+            slot_ = o.slot_;
+            o.slot_ = kNoSlot;
+        }
+        return *this;
+    }
 
     // rc4_encryption.h:46-72 -- the key is taken by value as a std::string, so
     // embedded NULs count (length(), not strlen) and an empty key means the
     // identity box with x = y = 0.
     void makeSBox(std::string obscure)
     {
-        zrc4_throw(zrc4_make_sbox(Rc4Arena::instance().ctx(), slot_,
+        zrc4_throw(zrc4_make_sbox(Rc4Arena::instance().ctx(slot_), Rc4Arena::local(slot_),
                                   reinterpret_cast<const uint8_t *>(obscure.data()),
                                   obscure.size()),
                    "RC4Encryption::makeSBox");
@@ -95,23 +141,33 @@ public:
     // rc4_encryption.h:74-93 -- in place; length <= 0 does nothing.
     void encryption(unsigned char *data, int length)
     {
-        zrc4_throw(zrc4_encryption(Rc4Arena::instance().ctx(), slot_, data, length),
+        zrc4_throw(zrc4_encryption(Rc4Arena::instance().ctx(slot_), Rc4Arena::local(slot_), data, length),
                    "RC4Encryption::encryption");
     }
 
     uint32_t slot() const { return slot_; }
 
 private:
+    static constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+    void copyState(const RC4Encryption &o)
+    {
+        Rc4Arena &a = Rc4Arena::instance();
+        uint8_t sb[256], x = 0, y = 0;
+        zrc4_throw(zrc4_get_state(a.ctx(o.slot_), Rc4Arena::local(o.slot_), sb, &x, &y), "RC4Encryption copy");
+        zrc4_throw(zrc4_set_state(a.ctx(slot_), Rc4Arena::local(slot_), sb, x, y), "RC4Encryption copy");
+    }
     uint32_t slot_;
 };
 
 // Batched hook path: collect (slot, buffer, len) for one event-loop
 // iteration, then crypt them all with one launch.  Host buffers are gathered
 // into one pinned staging copy by zrc4_crypt_host.  Entries are crypted in
-// insertion order per slot; a slot may appear once per flush.
+// insertion order per slot; a slot may appear once per flush.  `slot` is a
+// slot of `ctx` (for RC4Encryption objects: Rc4Arena::local(r.slot()) of
+// the chunk Rc4Arena::instance().ctx(r.slot())).
 class Rc4Batch {
 public:
-    explicit Rc4Batch(zrc4_ctx *ctx = Rc4Arena::instance().ctx()) : ctx_(ctx) {}
+    explicit Rc4Batch(zrc4_ctx *ctx) : ctx_(ctx) {}
     void add(uint32_t slot, unsigned char *data, unsigned len)
     {
         if (!len) return;

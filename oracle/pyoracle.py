@@ -52,6 +52,8 @@ def lib():
         L.oracle_state_to_bytes.argtypes = [_P, _P, _P, _P]
         L.oracle_state_from_bytes.argtypes = [_P, _P, C.c_uint8, C.c_uint8]
         L.oracle_now.restype = C.c_double
+        L.oracle_crypt_rate.argtypes = [_P, _P, _P, _P, C.c_uint32, C.c_int, C.c_double]
+        L.oracle_crypt_rate.restype = C.c_double
         L.oracle_frame_scan.argtypes = [_P, _P, _P, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P]
         _lib = L
     return _lib
@@ -183,6 +185,17 @@ class Batch:
         lib().oracle_crypt_batch(self.st, C.c_void_p(payload.ctypes.data),
                                  C.c_void_p(off.ctypes.data), C.c_void_p(length.ctypes.data),
                                  self.n, int(threads))
+
+    def crypt_rate(self, payload: np.ndarray, off: np.ndarray, length: np.ndarray, threads: int,
+                   seconds: float) -> float:
+        """Bytes/s of `threads` workers re-crypting their share for `seconds`."""
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        r = lib().oracle_crypt_rate(self.st, C.c_void_p(payload.ctypes.data), C.c_void_p(off.ctypes.data),
+                                    C.c_void_p(length.ctypes.data), self.n, int(threads), float(seconds))
+        if r < 0:
+            raise RuntimeError("oracle_crypt_rate: thread setup failed")
+        return r
 
     def state(self, i: int):
         sb = (C.c_uint8 * 256)()

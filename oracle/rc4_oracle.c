@@ -11,6 +11,7 @@
 #include "rc4_oracle.h"
 
 #include <pthread.h>
+#include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
@@ -105,6 +106,87 @@ void oracle_crypt_batch(oracle_rc4_state *st, uint8_t *payload,
     }
     for (int t = 0; t < threads; ++t)
         pthread_join(tids[t], NULL);
+}
+
+/* CPU-baseline timing (bench.py cpu_baseline): `threads` workers, each
+ * re-crypting its round-robin share of the n sessions pass after pass until
+ * `seconds` have elapsed (one thread start per worker, not per pass).
+ * Returns payload bytes per second over the wall time from the common start
+ * to the last worker's finish. */
+typedef struct {
+    crypt_job job;
+    pthread_barrier_t *bar;
+    double deadline;
+    unsigned long long bytes;
+} timed_job;
+
+static void *timed_worker(void *arg)
+{
+    timed_job *t = (timed_job *)arg;
+    crypt_job *j = &t->job;
+    pthread_barrier_wait(t->bar);
+    unsigned long long bytes = 0;     /* local: the job records share cache lines */
+    /* a contiguous share per worker: neighbouring states (1032 B each) and
+     * payloads then belong to the same worker, no cache line ping-pong */
+    const uint32_t lo = (uint32_t)((uint64_t)j->n * (uint32_t)j->tid / (uint32_t)j->nthreads);
+    const uint32_t hi = (uint32_t)((uint64_t)j->n * ((uint32_t)j->tid + 1u) / (uint32_t)j->nthreads);
+    do {
+        for (uint32_t i = lo; i < hi; ++i) {
+            oracle_encryption(&j->st[i], j->payload + j->off[i], (long)j->len[i]);
+            bytes += j->len[i];
+        }
+    } while (oracle_now() < t->deadline);
+    t->bytes = bytes;
+    return NULL;
+}
+
+double oracle_crypt_rate(oracle_rc4_state *st, uint8_t *payload, const uint64_t *off, const uint32_t *len,
+                         uint32_t n, int threads, double seconds)
+{
+    if (threads < 1)
+        threads = 1;
+    if ((uint32_t)threads > n)
+        threads = (int)n;
+    pthread_t *tids = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    timed_job *jobs = (timed_job *)calloc((size_t)threads, sizeof(timed_job));
+    pthread_barrier_t bar;
+    if (!tids || !jobs || pthread_barrier_init(&bar, NULL, (unsigned)threads + 1) != 0) {
+        free(tids);
+        free(jobs);
+        return -1.0;
+    }
+    int started = 0;
+    for (int t = 0; t < threads; ++t) {
+        crypt_job j = {st, payload, off, len, n, t, threads};
+        jobs[t].job = j;
+        jobs[t].bar = &bar;
+        jobs[t].deadline = 0.0;
+        jobs[t].bytes = 0;
+    }
+    /* deadline set before the start, read by workers only after the barrier */
+    for (int t = 0; t < threads; ++t) {
+        if (pthread_create(&tids[t], NULL, timed_worker, &jobs[t]) != 0)
+            break;
+        ++started;
+    }
+    if (started != threads) {   /* cannot release the barrier: give up */
+        abort();
+    }
+    const double t0 = oracle_now();
+    for (int t = 0; t < threads; ++t)
+        jobs[t].deadline = t0 + seconds;
+    pthread_barrier_wait(&bar);
+    const double tb = oracle_now();
+    unsigned long long bytes = 0;
+    for (int t = 0; t < threads; ++t) {
+        pthread_join(tids[t], NULL);
+        bytes += jobs[t].bytes;
+    }
+    const double t1 = oracle_now();
+    pthread_barrier_destroy(&bar);
+    free(tids);
+    free(jobs);
+    return (double)bytes / (t1 - tb);
 }
 
 void oracle_state_to_bytes(const oracle_rc4_state *st, uint8_t sbox[256],

@@ -66,6 +66,11 @@ void oracle_frame_scan(const uint8_t *buf, const uint64_t *off, const uint32_t *
 /* Wall-clock seconds (CLOCK_MONOTONIC) for the cpu_baseline timer. */
 double oracle_now(void);
 
+/* CPU-baseline timing: payload bytes per second of `threads` workers
+ * re-crypting their contiguous share of the n sessions for `seconds`. */
+double oracle_crypt_rate(oracle_rc4_state *st, uint8_t *payload, const uint64_t *off, const uint32_t *len,
+                         uint32_t n, int threads, double seconds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,37 @@ int zrc4_crypt(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_
     }
     return ZRC4_OK;
 }
+// Same contract checks as crypt_kernel<kGrouped>: a bucket's busy entries
+// must share one group (else the bucket is skipped and ZRC4_ERR_GROUP reported).
+int zrc4_crypt_grouped(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_t *off,
+                       const uint32_t *len, uint32_t n, void *)
+{
+    int rc = ZRC4_OK;
+    for (uint32_t b = 0; b < n; b += 256) {
+        const uint32_t e = b + 256 < n ? b + 256 : n;
+        uint32_t gmin = 0xFFFFFFFFu, gmax = 0;
+        for (uint32_t i = b; i < e; ++i) {
+            if (!len[i] || ids[i] == ZRC4_IDLE_SLOT) continue;
+            if (ids[i] >= c->st.size()) return ZRC4_ERR_SLOT_RANGE;
+            gmin = ids[i] / 256 < gmin ? ids[i] / 256 : gmin;
+            gmax = ids[i] / 256 > gmax ? ids[i] / 256 : gmax;
+        }
+        if (gmin != 0xFFFFFFFFu && gmin != gmax) {
+            rc = ZRC4_ERR_GROUP;
+            continue;
+        }
+        for (uint32_t i = b; i < e; ++i)
+            if (len[i] && ids[i] != ZRC4_IDLE_SLOT) oracle_encryption(&c->st[ids[i]], payload + off[i], (long)len[i]);
+    }
+    return rc;
+}
+int zrc4_crypt_grouped_frame(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_t *off,
+                             const uint32_t *len, uint32_t n, const zrc4_frame_args *f, void *s)
+{
+    const int rc = zrc4_crypt_grouped(c, ids, payload, off, len, n, s);
+    oracle_frame_scan(payload, f->off, f->len, f->bound, n, f->max_packets, f->npk, f->used, f->status, f->pkt_len);
+    return rc;
+}
 int zrc4_xor_ring(zrc4_ctx *, uint8_t *ring, uint32_t cap, const uint32_t *rid, const uint32_t *pos,
                   uint8_t *payload, const uint64_t *off, const uint32_t *len, uint32_t n, void *)
 {
@@ -127,4 +158,5 @@ hipError_t hipEventQuery(hipEvent_t)
     static unsigned k;
     return (++k % 3) ? hipErrorNotReady : hipSuccess;
 }
+hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
 hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }

@@ -4,7 +4,9 @@
 // crypt() over random spans inside pooled blocks, reseeding some sessions on
 // the way -- and checks every byte against the oracle RC4
 // (oracle/rc4_oracle.c, pinned to rc4_encryption.h:46-93).
-//   usage: hooks_check [device|direct] [sessions] [rounds] [seed]
+//   usage: hooks_check [device|direct] [sessions] [rounds] [seed] [ring bytes]
+// (a small ring forces ring wrap-around, partial ring coverage and tail
+// crypts on most calls).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -12,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "zrc4.h"
 #include "zsummerx_amd/rc4_hooks.h"
 extern "C" {
 #include "rc4_oracle.h"
@@ -26,7 +29,8 @@ int main(int argc, char **argv)
     const int rounds = argc > 3 ? std::atoi(argv[3]) : 200;
     std::mt19937 rng(argc > 4 ? std::atoi(argv[4]) : 1);
     const uint32_t slots = 2 * S;
-    std::unique_ptr<Rc4Hooks> h = makeDeviceRc4Hooks(0, slots, mode == "direct" ? 0u : 32768u);
+    const uint32_t ring = argc > 5 ? (uint32_t)std::atoi(argv[5]) : 32768u;
+    std::unique_ptr<Rc4Hooks> h = makeDeviceRc4Hooks(0, slots, mode == "direct" ? 0u : ring);
     const size_t blk = 20544;
     uint8_t *pool = static_cast<uint8_t *>(h->allocBlocks(slots * blk + 64));
     std::vector<oracle_rc4_state> ref(slots);
@@ -75,8 +79,18 @@ int main(int argc, char **argv)
                 }
         }
     }
-    std::printf("{\"ok\": true, \"mode\": \"%s\", \"sessions\": %u, \"rounds\": %d, \"bytes\": %llu}\n", mode.c_str(),
-                S, rounds, bytes);
+    // a slot twice in one call is refused (rc4_hooks.h contract), state untouched
+    {
+        uint8_t *d = pool + 64;
+        const Rc4Span dup[2] = {{0, 16, d}, {0, 16, d + 32}};
+        const int rc = h->crypt(dup, 2);
+        if (rc != ZRC4_ERR_INVALID_ARG) {
+            std::printf("{\"ok\": false, \"duplicate_rc\": %d}\n", rc);
+            return 4;
+        }
+    }
+    std::printf("{\"ok\": true, \"mode\": \"%s\", \"sessions\": %u, \"rounds\": %d, \"bytes\": %llu, "
+                "\"hooks\": %s}\n", mode.c_str(), S, rounds, bytes, h->stats().c_str());
     h->freeBlocks(pool);
     return 0;
 }

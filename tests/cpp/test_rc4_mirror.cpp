@@ -11,6 +11,7 @@
 #include "zsummerx_amd/rc4_encryption.h"
 
 using zsummerx_amd::RC4Encryption;
+using zsummerx_amd::Rc4Arena;
 using zsummerx_amd::Rc4Batch;
 
 static int fails = 0;
@@ -82,15 +83,70 @@ int main()
             for (size_t j = 0; j < plain[i].size(); ++j) plain[i][j] = (unsigned char)(i * 131 + j * 7);
             wire[i] = plain[i];
         }
-        Rc4Batch send_batch, recv_batch;
-        for (int i = 0; i < kPeers; ++i) send_batch.add(cw[i].slot(), wire[i].data(), (unsigned)wire[i].size());
+        zrc4_ctx *ctx = Rc4Arena::instance().ctx(cw[0].slot());
+        for (int i = 0; i < kPeers; ++i) CHECK(cw[i].slot() / Rc4Arena::kChunk == 0 && sr[i].slot() / Rc4Arena::kChunk == 0);
+        Rc4Batch send_batch(ctx), recv_batch(ctx);
+        for (int i = 0; i < kPeers; ++i)
+            send_batch.add(Rc4Arena::local(cw[i].slot()), wire[i].data(), (unsigned)wire[i].size());
         CHECK(send_batch.flush() == ZRC4_OK);
         int differs = 0;
         for (int i = 0; i < kPeers; ++i) differs += wire[i] != plain[i];
         CHECK(differs == kPeers);
-        for (int i = 0; i < kPeers; ++i) recv_batch.add(sr[i].slot(), wire[i].data(), (unsigned)wire[i].size());
+        for (int i = 0; i < kPeers; ++i)
+            recv_batch.add(Rc4Arena::local(sr[i].slot()), wire[i].data(), (unsigned)wire[i].size());
         CHECK(recv_batch.flush() == ZRC4_OK);
         for (int i = 0; i < kPeers; ++i) CHECK(wire[i] == plain[i]);
+    }
+    // value semantics: a copy continues the same stream from the same point
+    {
+        RC4Encryption a;
+        a.makeSBox("Key");
+        unsigned char x[9] = {0};
+        a.encryption(x, 4);
+        RC4Encryption b(a), c;
+        c = a;
+        unsigned char p[5] = {0}, q[5] = {0}, r[5] = {0};
+        a.encryption(p, 5);
+        b.encryption(q, 5);
+        c.encryption(r, 5);
+        CHECK(std::memcmp(p, q, 5) == 0 && std::memcmp(p, r, 5) == 0);
+        unsigned char whole[9] = {0};
+        RC4Encryption d;
+        d.makeSBox("Key");
+        d.encryption(whole, 9);
+        CHECK(std::memcmp(whole + 4, q, 5) == 0);
+        RC4Encryption m(std::move(b));                 // move keeps the slot and its state
+        unsigned char t[3] = {0}, u[3] = {0};
+        m.encryption(t, 3);
+        c.encryption(u, 3);
+        CHECK(std::memcmp(t, u, 3) == 0);
+    }
+    // slots recycle with the empty-key state; more than one 65 536-stream chunk
+    {
+        uint32_t first;
+        {
+            RC4Encryption a;
+            a.makeSBox("something");
+            first = a.slot();
+        }
+        RC4Encryption b;                               // reuses a's slot, identity state
+        CHECK(b.slot() == first);
+        unsigned char x[8] = {0}, y[8] = {0};
+        b.encryption(x, 8);
+        RC4Encryption e;
+        e.makeSBox("");
+        e.encryption(y, 8);
+        CHECK(std::memcmp(x, y, 8) == 0);
+        std::vector<RC4Encryption> many(Rc4Arena::kChunk + 100);
+        CHECK(many.back().slot() >= Rc4Arena::kChunk);
+        many.back().makeSBox("Key");
+        std::vector<unsigned char> z(9, 0);
+        many.back().encryption(z.data(), 9);
+        CHECK(hex(z.data(), 9) != "000000000000000000");
+        unsigned char kp[9];
+        std::memcpy(kp, "Plaintext", 9);
+        for (int i = 0; i < 9; ++i) kp[i] ^= z[i];
+        CHECK(hex(kp, 9) == "BBF316E8D940AF0AD3");
     }
     std::printf(fails ? "FAILED %d\n" : "ok\n", fails);
     return fails ? 1 : 0;

@@ -125,8 +125,8 @@ def echo_client(port, seed, npk, results, idx, keyed=True):
     results[idx] = (plain, bytes(got), rd.encryption(bytes(got)))
 
 
-def run_echo_parity(stress, hooks, nclients=6, npk=40):
-    srv = Server(stress, hooks, nclients)
+def run_echo_parity(stress, hooks, nclients=6, npk=40, extra=()):
+    srv = Server(stress, hooks, nclients, *extra)
     results = [None] * nclients
     th = [threading.Thread(target=echo_client, args=(srv.port, 1000 + i, npk, results, i)) for i in range(nclients)]
     for t in th:
@@ -252,10 +252,10 @@ def run_flash_policy(stress, hooks):
     srv.finish()
 
 
-def run_corrupt_closes(stress, hooks):
+def run_corrupt_closes(stress, hooks, extra=()):
     """A length field below the 6-byte header is BCT_CORRUPTION: the session is
     closed (session.cpp:355-361), the peer sees EOF."""
-    srv = Server(stress, hooks, 1)
+    srv = Server(stress, hooks, 1, *extra)
     wr = rc4()
     with socket.create_connection(("127.0.0.1", srv.port), timeout=30) as s:
         s.sendall(wr.encryption(struct.pack("<IHH", 3, 0, 0)))
@@ -269,7 +269,10 @@ def run_corrupt_closes(stress, hooks):
 def stress_emu(built):
     """The engine with the DEVICE hooks' host logic (keystream reservoirs) over a
     CPU emulation of the zrc4 C-ABI (tests/cpp/emu_zrc4_hip.cpp)."""
+    import os
     from zsummerx_amd import build
+    if os.environ.get("ZSX_TOOLS_BIN"):            # scripts/sanitize.sh: ASan/UBSan builds
+        return __import__('pathlib').Path(os.environ["ZSX_TOOLS_BIN"]) / "frame_stress_emu"
     build.build_test_tools()
     return ROOT / "tools" / "bin" / "frame_stress_emu"
 
@@ -290,6 +293,17 @@ def test_engine_echo_parity_cpu_hooks(stress):
 def test_mixed_keyed_and_keyless_emulated_device_hooks(stress_emu):
     st = run_mixed_keyed_plain(stress_emu, "device")
     assert st["rc4"] == "zrc4-gfx950"
+
+
+def test_device_framing_emulated(stress_emu):
+    """Receive blocks framed in the decrypt launch (setDeviceFraming, direct
+    hooks): same wire bytes and packet stream as host framing."""
+    st = run_echo_parity(stress_emu, "device-direct", extra=("--device-framing",))
+    assert st["device_framed"] > 0
+
+
+def test_device_framing_corrupt_closes_emulated(stress_emu):
+    run_corrupt_closes(stress_emu, "device-direct", extra=("--device-framing",))
 
 
 def test_mixed_keyed_and_keyless_cpu_hooks(stress):
@@ -321,6 +335,8 @@ def test_no_device_is_loud(stress):
     import torch  # noqa: F401  (only to know whether a GPU exists here)
     if torch.cuda.is_available():
         pytest.skip("a GPU is present")
+    if stress.name.endswith("_emu"):
+        pytest.skip("ZSX_STRESS is the CPU emulation of the C-ABI (scripts/sanitize.sh)")
     p = subprocess.run([str(stress), "--rc4", "device", "--seconds", "0.1"], capture_output=True, text=True,
                        timeout=60)
     assert p.returncode == 1 and "gfx950" in p.stderr
@@ -343,6 +359,17 @@ def test_mixed_keyed_and_keyless_device(stress):
 def test_mixed_keyed_and_keyless_device_direct(stress):
     st = run_mixed_keyed_plain(stress, "device-direct")
     assert st["rc4"] == "zrc4-gfx950-direct"
+
+
+@pytest.mark.gpu
+def test_device_framing_echo_parity_device(stress):
+    st = run_echo_parity(stress, "device-direct", extra=("--device-framing",))
+    assert st["rc4"] == "zrc4-gfx950-direct" and st["device_framed"] > 0
+
+
+@pytest.mark.gpu
+def test_device_framing_corrupt_closes_device(stress):
+    run_corrupt_closes(stress, "device-direct", extra=("--device-framing",))
 
 
 @pytest.mark.gpu

@@ -163,3 +163,80 @@ def test_decrypt_then_scan_pipeline(built):
                status.cpu().numpy().view(np.uint32), pk.cpu().numpy().view(np.uint32).reshape(n, 8))
     for w, g, name in zip(want, got, ["npk", "used", "status", "pkt_len"]):
         assert np.array_equal(w, g), name
+
+
+def _fused_case(n, avg, seed, tail_frac=0.5):
+    """Receive blocks as onRecv sees them: the first part of each block was
+    decrypted by an earlier iteration (plaintext already), the rest is the
+    fresh ciphertext tail (session.cpp:315-323).  Returns plaintext blocks,
+    the device input, the decrypt spans and the per-session keys."""
+    buf, off, ln = packet_streams(n, avg, seed=seed)
+    rng = np.random.default_rng(seed)
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(n)]
+    head = (ln * rng.uniform(0, tail_frac, n)).astype(np.uint32)      # already-decrypted prefix
+    inp = buf.copy()
+    for i in range(n):
+        a, z = int(off[i] + head[i]), int(off[i] + ln[i])
+        inp[a:z] = np.frombuffer(pyoracle.Rc4(keys[i]).encryption(inp[a:z].tobytes()), np.uint8)
+    return buf, inp, off, ln, off + head, ln - head, keys
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,avg,mode", [(4096, 900, "range"), (1000, 3000, "grouped"), (70000, 200, "range")])
+def test_fused_decrypt_and_frame(built, n, avg, mode):
+    """zrc4_crypt_*_frame: decrypt the fresh tail and frame the WHOLE block in
+    one launch (fused epilogue at <= 1 group per CU; the 70 000-session case
+    exceeds one group per CU and takes the throughput kernel + scan launch).
+    Plaintext and framing against the oracle."""
+    import torch
+    from zsummerx_amd import Context
+    from zsummerx_amd._capi import IDLE_SLOT
+    maxp = 8
+    buf, inp, off, ln, toff, tlen, keys = _fused_case(n, avg, seed=n + avg)
+    want = pyoracle.frame_scan(buf, off, ln, BOUND, maxp)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+    npk, used, status = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    pk = torch.zeros(n * maxp, dtype=torch.int32, device="cuda")
+    d = T(inp)
+    frame = {"off": T(off.view(np.int64)), "len": T(ln.view(np.int32)), "bound": BOUND, "max_packets": maxp,
+             "npk": npk, "used": used, "status": status, "pkt_len": pk}
+    with Context(0, n + 512) as c:
+        if mode == "range":
+            c.ksa_host(keys)
+            c.crypt_range_frame(0, d, T(toff.view(np.int64)), T(tlen.view(np.int32)), frame)
+        else:
+            # slots scattered over groups, entries bucketed by group (zrc4_crypt_grouped contract)
+            rng = np.random.default_rng(5)
+            slots = rng.permutation(n + 512)[:n].astype(np.uint32)
+            c.ksa_host(keys, ids=slots)
+            order = np.argsort(slots, kind="stable")
+            ids, eo, el, fo, fl, back = [], [], [], [], [], []
+            cur = None
+            for i in order:
+                g = int(slots[i]) // 256
+                if g != cur:
+                    while len(ids) % 256:
+                        ids.append(IDLE_SLOT); eo.append(0); el.append(0); fo.append(0); fl.append(0); back.append(-1)
+                    cur = g
+                ids.append(int(slots[i])); eo.append(int(toff[i])); el.append(int(tlen[i]))
+                fo.append(int(off[i])); fl.append(int(ln[i])); back.append(int(i))
+            m = len(ids)
+            npk, used, status = (torch.zeros(m, dtype=torch.int32, device="cuda") for _ in range(3))
+            pk = torch.zeros(m * maxp, dtype=torch.int32, device="cuda")
+            frame.update(off=T(np.array(fo, np.uint64).view(np.int64)), len=T(np.array(fl, np.uint32).view(np.int32)),
+                         npk=npk, used=used, status=status, pkt_len=pk)
+            c.crypt_grouped_frame(d, T(np.array(eo, np.uint64).view(np.int64)),
+                                  T(np.array(el, np.uint32).view(np.int32)),
+                                  T(np.array(ids, np.uint32).view(np.int32)), frame)
+        c.sync()
+        assert np.array_equal(d.cpu().numpy(), buf)
+        got = [npk.cpu().numpy().view(np.uint32), used.cpu().numpy().view(np.uint32),
+               status.cpu().numpy().view(np.uint32), pk.cpu().numpy().view(np.uint32).reshape(-1, maxp)]
+        if mode == "grouped":
+            back = np.array(back)
+            sel = back >= 0
+            perm = np.empty(n, dtype=np.int64)
+            perm[back[sel]] = np.flatnonzero(sel)
+            got = [g[perm] for g in got]
+    for w, g, name in zip(want, got, ["npk", "used", "status", "pkt_len"]):
+        assert np.array_equal(w, g), name

@@ -70,13 +70,15 @@ def test_edge_cases(ctx, edge):
 
 
 def test_ksa_key_lengths_batched(built, torch_cuda):
-    """Batched makeSBox over key lengths 0..40, 64, 255, 256, 257, 300 (the
-    register-pattern path takes lengths 1, 2, 4, 8, 16; every other length
-    fetches key bytes per step), NUL bytes included, keys at odd offsets;
-    whole groups (range) and scattered ids; states against the oracle."""
+    """Batched makeSBox over key lengths 0..40, 63, 64, 65, 128, 255, 256,
+    257, 300: the 16-byte register pattern takes lengths 1, 2, 4, 8, 16, the
+    64-byte register pattern 32 and 64, every other length (65 and 128 pin
+    the edges of the 64-byte branch) fetches key bytes per step; NUL bytes
+    included, keys at odd offsets; whole groups (range) and scattered ids;
+    states against the oracle."""
     torch = torch_cuda
     rng = np.random.default_rng(31)
-    lens = list(range(0, 41)) + [64, 255, 256, 257, 300]
+    lens = list(range(0, 41)) + [63, 64, 65, 128, 255, 256, 257, 300]
     n = 512
     klen = np.array([lens[i % len(lens)] for i in range(n)], dtype=np.uint32)
     koff = (np.concatenate([[3], np.cumsum(klen[:-1] + 1) + 3])).astype(np.uint64)
@@ -107,6 +109,25 @@ def test_rc4encryption_mirror_class(built, kat):
     assert data.hex() == v["ciphertext"]
     r.encryption(data, 0)            # no-op
     r.encryption(data, -3)           # no-op (reference: length <= 0)
+
+
+def test_rc4encryption_mirror_recycles_slots(built):
+    """Instances give their slot back (per-context free list): a 256-slot
+    context serves 1 000 short-lived instances, a recycled slot starts from
+    the empty-key state, and live instances never share a slot."""
+    with Context(0, 256) as c:
+        live = [RC4Encryption(c) for _ in range(200)]
+        assert len({r.slot for r in live}) == 200
+        for _ in range(1000):
+            r = RC4Encryption(c)
+            r.makeSBox("temporary")
+            r.encryption(bytearray(64), 64)
+            r.close()
+        r = RC4Encryption(c)
+        assert c.get_state(r.slot) == (bytes(range(256)), 0, 0)
+        with pytest.raises(ZRC4Error):
+            _ = [RC4Encryption(c) for _ in range(100)]      # 200 + 1 + 100 > 256 live
+        del live
 
 
 # ----------------------------------------------------------- batched, ragged
@@ -328,6 +349,96 @@ def test_direct_path_block_edges(built, torch_cuda, first_slot):
             sb, x, y = c.get_state(first_slot + i)
             want_sb, wx, wy = ob.state(i)
             assert (sb, x, y) == (bytes(want_sb), wx, wy), i
+
+
+# ------------------------------------------ grouped ids (zrc4_crypt_grouped)
+def grouped_batch(rng, n_groups, groups_total, fill=(1, 256)):
+    """Buckets of 256 entries: bucket b takes a random subset (random order)
+    of group g_b's slots, groups drawn without repetition; padding entries
+    are ZRC4_IDLE_SLOT.  Returns (ids[n], member_index[n] or -1)."""
+    from zsummerx_amd._capi import IDLE_SLOT
+    groups = rng.permutation(groups_total)[:n_groups]
+    ids = np.full(256 * n_groups, IDLE_SLOT, dtype=np.uint32)
+    for b, g in enumerate(groups):
+        k = int(rng.integers(fill[0], fill[1] + 1))
+        slots = g * 256 + rng.permutation(256)[:k]
+        pos = rng.permutation(256)[:k]
+        ids[256 * b + pos] = slots
+    return ids
+
+
+@pytest.mark.parametrize("fill", [(256, 256), (1, 256)])
+def test_grouped_ids_bit_exact(built, torch_cuda, fill):
+    """zrc4_crypt_grouped: each bucket a subset of ONE group, in any order,
+    groups in random order, idle padding; two calls in a row continue the
+    keystream.  Checked against the oracle, every session that ran and every
+    state; slots outside the batch keep their state."""
+    torch = torch_cuda
+    from zsummerx_amd._capi import IDLE_SLOT
+    rng = np.random.default_rng(41 + fill[0])
+    G, nb = 96, 64                                 # 96 groups in the arena, 64 buckets per call
+    cap = 256 * G
+    keys = rng.integers(0, 256, 16 * cap, dtype=np.uint8)
+    koff = np.arange(cap, dtype=np.uint64) * 16
+    klen = np.full(cap, 16, dtype=np.uint32)
+    ob = pyoracle.Batch(cap)
+    ob.make_sbox(keys, koff, klen)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    s = torch.cuda.current_stream()
+    with Context(0, cap) as c:
+        c.ksa_range(0, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
+        touched = set()
+        for call in range(2):
+            ids = grouped_batch(rng, nb, G, fill)
+            busy = ids != IDLE_SLOT
+            L = np.where(busy, rng.integers(0, 600, ids.size), 0).astype(np.uint32)
+            off = (np.arange(ids.size, dtype=np.uint64) * 640 + rng.integers(0, 16, ids.size).astype(np.uint64))
+            data = rng.integers(0, 256, ids.size * 640 + 64, dtype=np.uint8)
+            # oracle: per slot, in batch order (each slot once per call)
+            want = data.copy()
+            for e in np.flatnonzero(busy):
+                st = ob.st[int(ids[e])]
+                pyoracle.lib().oracle_encryption(pyoracle.C.byref(st),
+                                                 pyoracle.C.c_void_p(want.ctypes.data + int(off[e])), int(L[e]))
+            touched.update(int(v) for v in ids[busy])
+            pay = T(data)
+            c.crypt_grouped(pay, T(off.view(np.int64)), T(L.view(np.int32)), T(ids.view(np.int32)), stream=s)
+            c.sync(s)
+            got = pay.cpu().numpy()
+            bad = np.flatnonzero(got != want)
+            assert bad.size == 0, (call, bad[:8], int(bad.size))
+        for slot in list(touched)[:40] + [v for v in range(0, cap, 997) if v not in touched][:20]:
+            sb, x, y = c.get_state(slot)
+            want_sb, wx, wy = ob.state(slot)
+            assert (sb, x, y) == (bytes(want_sb), wx, wy), slot
+
+
+def test_grouped_ids_mixed_bucket_is_refused(built, torch_cuda):
+    """A bucket whose busy entries span two groups is skipped whole (no byte
+    or state touched) and reported as ZRC4_ERR_GROUP; other buckets run."""
+    torch = torch_cuda
+    from zsummerx_amd._capi import IDLE_SLOT
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    s = torch.cuda.current_stream()
+    with Context(0, 1024) as c:
+        c.ksa_host([b"key-%d" % i for i in range(1024)], ids=np.arange(1024, dtype=np.uint32))
+        ids = np.full(512, IDLE_SLOT, dtype=np.uint32)
+        ids[0], ids[1] = 5, 300                      # bucket 0: groups 0 and 1 -> refused
+        ids[256], ids[257] = 700, 701                # bucket 1: group 2 -> runs
+        L = np.where(ids != IDLE_SLOT, 32, 0).astype(np.uint32)
+        off = np.arange(512, dtype=np.uint64) * 32
+        pay = T(np.zeros(512 * 32, dtype=np.uint8))
+        before = [c.get_state(v) for v in (5, 300)]
+        c.crypt_grouped(pay, T(off.view(np.int64)), T(L.view(np.int32)), T(ids.view(np.int32)), stream=s)
+        with pytest.raises(ZRC4Error) as ei:
+            c.sync(s)
+        assert ei.value.code == -7
+        got = pay.cpu().numpy()
+        assert not got[:2 * 32].any()                # refused bucket: payload untouched
+        assert got[256 * 32: 258 * 32].any()          # bucket 1 ran
+        assert [c.get_state(v) for v in (5, 300)] == before
+        ks = pyoracle.Rc4(b"key-700").encryption(bytes(32))
+        assert got[256 * 32: 257 * 32].tobytes() == ks
 
 
 # ------------------------------------------------ full BASELINE-size configs

@@ -20,7 +20,11 @@ BIN = ROOT / "tools" / "bin"
 
 @pytest.fixture(scope="module")
 def tools(built):
+    import os
+    from pathlib import Path
     from zsummerx_amd import build
+    if os.environ.get("ZSX_TOOLS_BIN"):            # scripts/sanitize.sh: ASan/UBSan builds
+        return Path(os.environ["ZSX_TOOLS_BIN"])
     build.build_test_tools()
     return BIN
 
@@ -38,6 +42,13 @@ def test_reservoir_host_logic_emulated(tools, seed):
     run(tools / "hooks_check_emu", "device", 48, 150, seed)
 
 
+@pytest.mark.parametrize("ring", [256, 1000, 4096])
+def test_reservoir_small_rings_emulated(tools, ring):
+    # rings far below the span sizes: wrap-around, partial coverage + tail crypts
+    out = run(tools / "hooks_check_emu", "device", 40, 120, 5, ring)
+    assert out["hooks"]["tail_bytes"] > 0 and out["hooks"]["ring_bytes"] > 0
+
+
 def test_direct_host_logic_emulated(tools):
     run(tools / "hooks_check_emu", "direct", 16, 40, 9)
 
@@ -47,6 +58,12 @@ def test_direct_host_logic_emulated(tools):
                                                         ("direct", 64, 80, 2)])
 def test_device_hooks_vs_oracle(tools, mode, sessions, rounds, seed):
     run(tools / "hooks_check", mode, sessions, rounds, seed)
+
+
+@pytest.mark.gpu
+def test_device_hooks_small_ring(tools):
+    out = run(tools / "hooks_check", "device", 96, 150, 11, 1000)
+    assert out["hooks"]["tail_bytes"] > 0 and out["hooks"]["ring_bytes"] > 0
 
 
 @pytest.mark.gpu

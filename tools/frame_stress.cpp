@@ -111,8 +111,9 @@ struct Args {
     unsigned echoes = 0;          // client: close a session after this many echoes (0 = run by time)
     bool flashPolicy = false;
     bool plainAccepter = false;   // server: a second accepter with RC4 off (empty key, config.h:196)
+    bool deviceFraming = false;   // frame receive blocks in the decrypt launch (direct device hooks)
     int device = 0;
-    unsigned ring = 32768;        // keystream reservoir bytes per slot (device hooks)
+    unsigned ring = 65536;        // keystream reservoir bytes per slot (device hooks)
 };
 
 double now()
@@ -179,6 +180,7 @@ static int run(int argc, char **argv)
         else if (k == "--echoes") a.echoes = (unsigned)std::stoul(val());
         else if (k == "--flash-policy") a.flashPolicy = true;
         else if (k == "--plain-accepter") a.plainAccepter = true;
+        else if (k == "--device-framing") a.deviceFraming = true;
         else if (k == "--device") a.device = std::stoi(val());
         else if (k == "--ring") a.ring = (unsigned)std::stoul(val());
         else {
@@ -202,6 +204,7 @@ static int run(int argc, char **argv)
         std::fprintf(stderr, "--rc4 must be device, device-direct, host:<lib> or off\n");
         return 2;
     }
+    mgr.setDeviceFraming(a.deviceFraming);
     mgr.start();
 
     unsigned long long mismatches = 0, closed = 0, linked = 0;
@@ -324,12 +327,13 @@ static int run(int argc, char **argv)
         "\"rc4_calls\": %.0f, \"rc4_spans\": %.0f, \"rc4_bytes\": %.0f, \"rc4_ms\": %.3f, "
         "\"rc4_us_per_call\": %.3f, \"spans_per_call\": %.2f, \"rc4_gib_s_inside_hooks\": %.4f, "
         "\"recv_bytes\": %.0f, \"send_bytes\": %.0f, \"recv_packs\": %.0f, \"iterations\": %llu, "
-        "\"mismatches\": %llu, \"linked\": %llu, \"closed\": %llu}\n",
+        "\"device_framed\": %.0f, \"mismatches\": %llu, \"linked\": %llu, \"closed\": %llu, \"hooks\": %s}\n",
         a.mode.c_str(), mgr.rc4Hooks() ? mgr.rc4Hooks()->name() : "none", a.sessions, a.block, a.depth, dt,
         e1 - e0, (double)(e1 - e0) / dt, calls, d(STAT_RC4_SPANS), d(STAT_RC4_BYTES), d(STAT_RC4_NANOS) * 1e-6,
         calls > 0 ? d(STAT_RC4_NANOS) * 1e-3 / calls : 0.0, calls > 0 ? d(STAT_RC4_SPANS) / calls : 0.0,
         d(STAT_RC4_NANOS) > 0 ? d(STAT_RC4_BYTES) / (d(STAT_RC4_NANOS) * 1e-9) / 1073741824.0 : 0.0,
-        d(STAT_RECV_BYTES), d(STAT_SEND_BYTES), d(STAT_RECV_PACKS), iters, mismatches, linked, closed);
+        d(STAT_RECV_BYTES), d(STAT_SEND_BYTES), d(STAT_RECV_PACKS), iters, d(STAT_RC4_FRAMED), mismatches, linked, closed,
+        mgr.rc4Hooks() ? mgr.rc4Hooks()->stats().c_str() : "{}");
     std::fflush(stdout);
     return mismatches ? 3 : 0;
 }

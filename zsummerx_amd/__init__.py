@@ -18,12 +18,13 @@ import threading
 
 import numpy as np
 
-from ._capi import ZRC4Error, check, load
+from ._capi import FrameArgs, ZRC4Error, check, load
 
 __all__ = ["Context", "RC4Encryption", "ZRC4Error", "load", "default_context"]
 
 GROUP_SLOTS = 256
 STATE_BYTES = 258
+_IDENTITY = bytes(range(256))
 
 
 def _ptr(a) -> C.c_void_p | None:
@@ -58,6 +59,30 @@ class Context:
         self._h = h
         self.device = int(device)
         self.capacity = int(self._lib.zrc4_capacity(h))
+        # slot allocator of the RC4Encryption mirror: per context, with a free list
+        self._slot_lock = threading.Lock()
+        self._free_slots: list[int] = []
+        self._next_slot = 0
+
+    # -- slot allocation (RC4Encryption instances) ---------------------------
+    def acquire_slot(self) -> int:
+        with self._slot_lock:
+            if self._free_slots:
+                return self._free_slots.pop()
+            if self._next_slot >= self.capacity:
+                raise ZRC4Error(-5, "RC4Encryption: context out of slots")
+            self._next_slot += 1
+            return self._next_slot - 1
+
+    def release_slot(self, slot: int) -> None:
+        """Give a slot back; it is reset to the empty-key state (identity box,
+        x = y = 0: what makeSBox("") leaves, rc4_encryption.h:48-56) so a
+        later owner never sees the previous owner's stream."""
+        if not getattr(self, "_h", None):
+            return
+        self.set_state(slot, _IDENTITY, 0, 0)
+        with self._slot_lock:
+            self._free_slots.append(int(slot))
 
     # -- lifetime ---------------------------------------------------------
     def close(self) -> None:
@@ -103,6 +128,25 @@ class Context:
         n = int(length.numel() if n is None else n)
         check(self._lib.zrc4_crypt_grouped(self._h, _ptr(ids), _ptr(payload), _ptr(off), _ptr(length),
                                            n, _stream(stream)), "zrc4_crypt_grouped")
+
+    @staticmethod
+    def _frame(frame: dict) -> FrameArgs:
+        return FrameArgs(_ptr(frame["off"]), _ptr(frame["len"]), int(frame["bound"]), int(frame.get("max_packets", 0)),
+                         _ptr(frame["npk"]), _ptr(frame["used"]), _ptr(frame["status"]), _ptr(frame.get("pkt_len")))
+
+    def crypt_range_frame(self, first_slot: int, payload, off, length, frame: dict, n=None, stream=None) -> None:
+        """zrc4_crypt_range_frame: decrypt + proto4z framing in one launch.
+        frame = {off, len, bound, npk, used, status[, pkt_len, max_packets]}."""
+        n = int(length.numel() if n is None else n)
+        fa = self._frame(frame)
+        check(self._lib.zrc4_crypt_range_frame(self._h, int(first_slot), _ptr(payload), _ptr(off), _ptr(length), n,
+                                               C.byref(fa), _stream(stream)), "zrc4_crypt_range_frame")
+
+    def crypt_grouped_frame(self, payload, off, length, ids, frame: dict, n=None, stream=None) -> None:
+        n = int(length.numel() if n is None else n)
+        fa = self._frame(frame)
+        check(self._lib.zrc4_crypt_grouped_frame(self._h, _ptr(ids), _ptr(payload), _ptr(off), _ptr(length), n,
+                                                 C.byref(fa), _stream(stream)), "zrc4_crypt_grouped_frame")
 
     def xor_ring(self, ring, ring_cap: int, rid, pos, payload, off, length, n=None, stream=None) -> None:
         """zrc4_xor_ring: payload spans ^= keystream rings (consumed bytes zeroed)."""
@@ -181,7 +225,6 @@ class Context:
 
 _default = None
 _default_lock = threading.Lock()
-_next_slot = 0
 
 
 def default_context(capacity: int = 1 << 16) -> Context:
@@ -195,19 +238,17 @@ def default_context(capacity: int = 1 << 16) -> Context:
 class RC4Encryption:
     """Drop-in mirror of the reference class (rc4_encryption.h:43-99).
 
-    Each instance owns one slot of the process-wide default context.  Like the
-    reference, a fresh instance must be seeded with makeSBox before use (the
-    reference leaves the state indeterminate; here a fresh slot is the
-    empty-key identity state)."""
+    Each instance owns one slot of a context (the process-wide default one
+    unless `ctx` is given) and gives it back when it is closed or collected,
+    so instances can come and go like the reference's value objects (two per
+    TcpSession, session.h:115-116).  Like the reference, a fresh instance must
+    be seeded with makeSBox before use (the reference leaves the state
+    indeterminate; here a fresh or recycled slot is the empty-key identity
+    state)."""
 
     def __init__(self, ctx: Context | None = None):
-        global _next_slot
         self._ctx = ctx or default_context()
-        with _default_lock:
-            if _next_slot >= self._ctx.capacity:
-                raise ZRC4Error(-5, "RC4Encryption: default context out of slots")
-            self._slot = _next_slot
-            _next_slot += 1
+        self._slot = self._ctx.acquire_slot()
 
     def makeSBox(self, obscure) -> None:  # noqa: N802  (reference name)
         self._ctx.make_sbox(self._slot, obscure)
@@ -218,3 +259,21 @@ class RC4Encryption:
     @property
     def slot(self) -> int:
         return self._slot
+
+    def close(self) -> None:
+        """Return the slot to the context (idempotent)."""
+        slot, self._slot = getattr(self, "_slot", None), None
+        if slot is not None:
+            self._ctx.release_slot(slot)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

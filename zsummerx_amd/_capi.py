@@ -36,6 +36,8 @@ SIGNATURES = [
     ("zrc4_ksa_range", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_crypt_range", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_crypt_grouped", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
+    ("zrc4_crypt_range_frame", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P]),
+    ("zrc4_crypt_grouped_frame", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P, _P]),
     ("zrc4_ksa_host", C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, C.c_uint32]),
     ("zrc4_crypt_host", C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, C.c_uint32]),
     ("zrc4_make_sbox", C.c_int, [_P, C.c_uint32, _P, C.c_size_t]),
@@ -48,6 +50,12 @@ SIGNATURES = [
     ("zrc4_strerror", C.c_char_p, [C.c_int]),
     ("zrc4_version", C.c_char_p, []),
 ]
+
+
+class FrameArgs(C.Structure):
+    """struct zrc4_frame_args (include/zrc4.h)."""
+    _fields_ = [("off", _P), ("len", _P), ("bound", C.c_uint32), ("max_packets", C.c_uint32),
+                ("npk", _P), ("used", _P), ("status", _P), ("pkt_len", _P)]
 
 
 class ZRC4Error(RuntimeError):

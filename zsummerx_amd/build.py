@@ -127,15 +127,20 @@ def build_frame(force: bool = False) -> Path:
     return FRAME
 
 
-def build_test_tools(force: bool = False) -> None:
+SANITIZE = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", "-g"]
+
+
+def build_test_tools(force: bool = False, sanitize: bool = False) -> Path:
     """Test infrastructure (links the oracle; never part of the product):
       tools/bin/hooks_check      the device Rc4Hooks driven like the engine,
                                  every byte checked against the oracle (GPU)
       tools/bin/hooks_check_emu  the same host logic over a CPU emulation of
                                  the zrc4 C-ABI (tests/cpp/emu_zrc4_hip.cpp)
-      tools/bin/frame_stress_emu the engine + device hooks over that emulation"""
+      tools/bin/frame_stress_emu the engine + device hooks over that emulation
+    sanitize=True builds only the two emulated binaries, with ASan + UBSan,
+    into tools/bin/san/ (scripts/sanitize.sh runs the CPU suites on them)."""
     frame = build_frame(force)
-    out = ROOT / "tools" / "bin"
+    out = ROOT / "tools" / "bin" / ("san" if sanitize else "")
     out.mkdir(parents=True, exist_ok=True)
     orc = ROOT / "oracle" / "liboracle.so"
     chk = ROOT / "tests" / "cpp" / "hooks_check.cpp"
@@ -156,9 +161,13 @@ def build_test_tools(force: bool = False) -> None:
          ["g++", "-O2", *common, *emu_flags, "-o", str(out / "frame_stress_emu"), str(ROOT / "tools" / "frame_stress.cpp"),
           *map(str, FRAME_SOURCES), str(emu), *oracle_link, "-ldl", "-lpthread"]),
     ]
+    if sanitize:
+        jobs = [(t, d, [c[0], *SANITIZE, *c[1:], "-Wl,-rpath,$ORIGIN/../../../oracle"])
+                for t, d, c in jobs if t.name.endswith("_emu")]
     for target, deps, cmd in jobs:
         if force or _stale(target, deps):
             subprocess.run(cmd, check=True)
+    return out
 
 
 def build_oracle() -> None:

@@ -66,19 +66,43 @@ int grow_stage(zrc4_ctx *c, size_t bytes)
 
 size_t align16(size_t v) { return (v + 15u) & ~(size_t)15u; }
 
+constexpr size_t kZeroCopyMax = 256u << 10;   // *_host batches up to this size run on pinned staging in place
+
 // Kernel choice per launch: more 256-slot groups than CUs -> the persistent
 // throughput kernel (2 workgroups per CU, whole-line stores through the DPP
 // transpose); otherwise one group per workgroup (crypt_kernel: chain-bound,
 // per-lane stores).  A/B: the DPP path is 5-7 us slower at one group per CU
 // (cfg2 56.1 vs 48.8 us, cfg3 28.1 vs 22.7 us; profiles/r02_ab_dpp_direct.log).
+// With `fr`, the framing walk of every entry runs too: fused into the direct
+// kernel's epilogue, or -- behind the throughput kernel -- as a second launch.
 int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot, uint8_t *payload,
-                 const uint64_t *off, const uint32_t *len, uint32_t n, hipStream_t s)
+                 const uint64_t *off, const uint32_t *len, uint32_t n, hipStream_t s,
+                 const zrc4::FrameArgs *fr = nullptr)
 {
     if (n == 0) return ZRC4_OK;
     if (mode == zrc4::kRange && (uint64_t)first_slot + n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
     const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
     const dim3 blk(zrc4::kGroup);
-    if (mode != zrc4::kGrouped && grid > (uint32_t)c->num_cus) {
+    const bool stream_kernel = mode != zrc4::kGrouped && grid > (uint32_t)c->num_cus;
+    if (fr && !stream_kernel) {
+        if (mode == zrc4::kRange)
+            hipLaunchKernelGGL((zrc4::crypt_kernel<zrc4::kRange, true>), dim3(grid), blk, 0, s, c->arena, c->xy,
+                               ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, *fr);
+        else if (mode == zrc4::kGrouped)
+            hipLaunchKernelGGL((zrc4::crypt_kernel<zrc4::kGrouped, true>), dim3(grid), blk, 0, s, c->arena, c->xy,
+                               ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, *fr);
+        else
+            return ZRC4_ERR_INVALID_ARG;
+        return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
+    }
+    if (fr) {
+        const int rc = launch_crypt(c, mode, ids, first_slot, payload, off, len, n, s, nullptr);
+        if (rc != ZRC4_OK) return rc;
+        hipLaunchKernelGGL(zrc4::frame_scan_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, payload, fr->off,
+                           fr->len, fr->bound, n, fr->maxp, fr->npk, fr->used, fr->status, fr->pkt_len);
+        return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
+    }
+    if (stream_kernel) {
         const uint32_t wgs = std::min(grid, 2u * (uint32_t)c->num_cus);
         if (mode == zrc4::kRange && (first_slot & 255u) == 0u)
             hipLaunchKernelGGL(zrc4::crypt_stream_kernel<true>, dim3(wgs), blk, 0, s, c->arena, c->xy, ids,
@@ -238,6 +262,48 @@ int zrc4_crypt_grouped(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const
     return launch_crypt(c, zrc4::kGrouped, ids, 0, payload, off, len, n, (hipStream_t)stream);
 }
 
+namespace {
+int frame_args(const zrc4_frame_args *f, uint32_t n, zrc4::FrameArgs &out)
+{
+    if (!f) return ZRC4_ERR_INVALID_ARG;
+    if (n && (!f->off || !f->len || !f->npk || !f->used || !f->status || (f->max_packets && !f->pkt_len)))
+        return ZRC4_ERR_INVALID_ARG;
+    out.off = f->off;
+    out.len = f->len;
+    out.bound = f->bound;
+    out.maxp = f->max_packets;
+    out.npk = f->npk;
+    out.used = f->used;
+    out.status = f->status;
+    out.pkt_len = f->max_packets ? f->pkt_len : nullptr;
+    return ZRC4_OK;
+}
+}  // namespace
+
+int zrc4_crypt_range_frame(zrc4_ctx *c, uint32_t first_slot, uint8_t *payload, const uint64_t *off,
+                           const uint32_t *len, uint32_t n, const zrc4_frame_args *frame, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n && (!payload || !off || !len)) return ZRC4_ERR_INVALID_ARG;
+    zrc4::FrameArgs fr;
+    int rc = frame_args(frame, n, fr);
+    if (rc) return rc;
+    if ((rc = set_device(c))) return rc;
+    return launch_crypt(c, zrc4::kRange, nullptr, first_slot, payload, off, len, n, (hipStream_t)stream, &fr);
+}
+
+int zrc4_crypt_grouped_frame(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_t *off,
+                             const uint32_t *len, uint32_t n, const zrc4_frame_args *frame, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n && (!ids || !payload || !off || !len)) return ZRC4_ERR_INVALID_ARG;
+    zrc4::FrameArgs fr;
+    int rc = frame_args(frame, n, fr);
+    if (rc) return rc;
+    if ((rc = set_device(c))) return rc;
+    return launch_crypt(c, zrc4::kGrouped, ids, 0, payload, off, len, n, (hipStream_t)stream, &fr);
+}
+
 int zrc4_xor_ring(zrc4_ctx *c, uint8_t *ring, uint32_t ring_cap, const uint32_t *rid,
                   const uint32_t *pos, uint8_t *payload, const uint64_t *off, const uint32_t *len,
                   uint32_t n, void *stream)
@@ -295,10 +361,15 @@ int zrc4_ksa_host(zrc4_ctx *c, const uint32_t *ids, const uint8_t *keys, size_t 
     memcpy(c->h_stage + o_off, key_off, (size_t)n * 8);
     memcpy(c->h_stage + o_len, key_len, (size_t)n * 4);
     if (keys_bytes) memcpy(c->h_stage + o_key, keys, keys_bytes);
-    ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
-    rc = launch_ksa(c, ids ? (const uint32_t *)(c->d_stage + o_ids) : nullptr, 0,
-                    c->d_stage + o_key, (const uint64_t *)(c->d_stage + o_off),
-                    (const uint32_t *)(c->d_stage + o_len), n, c->stream);
+    // Small batches run on the pinned staging copy in place (zero-copy over
+    // PCIe: one launch and one wait instead of copy + launch + wait).
+    uint8_t *st = c->h_stage;
+    if (total > kZeroCopyMax) {
+        ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
+        st = c->d_stage;
+    }
+    rc = launch_ksa(c, ids ? (const uint32_t *)(st + o_ids) : nullptr, 0,
+                    st + o_key, (const uint64_t *)(st + o_off), (const uint32_t *)(st + o_len), n, c->stream);
     if (rc) return rc;
     return check_err(c, c->stream);
 }
@@ -323,12 +394,19 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
     memcpy(c->h_stage + o_off, off, (size_t)n * 8);
     memcpy(c->h_stage + o_len, len, (size_t)n * 4);
     if (payload_bytes) memcpy(c->h_stage + o_pay, payload, payload_bytes);
-    ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
-    rc = launch_crypt(c, ids ? zrc4::kIds : zrc4::kRange, ids ? (const uint32_t *)(c->d_stage + o_ids) : nullptr, 0,
-                      c->d_stage + o_pay, (const uint64_t *)(c->d_stage + o_off),
-                      (const uint32_t *)(c->d_stage + o_len), n, c->stream);
+    // Small batches (the per-call RC4Encryption::encryption drop-in) run on
+    // the pinned staging copy in place: no H2D / D2H copies on the latency
+    // path.  Large ones are copied so the kernel streams HBM, not PCIe.
+    const bool zero_copy = total <= kZeroCopyMax;
+    uint8_t *st = c->h_stage;
+    if (!zero_copy) {
+        ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
+        st = c->d_stage;
+    }
+    rc = launch_crypt(c, ids ? zrc4::kIds : zrc4::kRange, ids ? (const uint32_t *)(st + o_ids) : nullptr, 0,
+                      st + o_pay, (const uint64_t *)(st + o_off), (const uint32_t *)(st + o_len), n, c->stream);
     if (rc) return rc;
-    if (payload_bytes)
+    if (payload_bytes && !zero_copy)
         ZRC4_TRY(hipMemcpyAsync(c->h_stage + o_pay, c->d_stage + o_pay, payload_bytes,
                                 hipMemcpyDeviceToHost, c->stream));
     rc = check_err(c, c->stream);

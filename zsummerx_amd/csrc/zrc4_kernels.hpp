@@ -662,13 +662,59 @@ __device__ __forceinline__ void issue_image_asm(u32x32 &ilo, u32x32 &ihi, const 
 // ---------------------------------------------------------------------------
 enum CryptMode : int { kIds = 0, kRange = 1, kGrouped = 2 };
 
-template <int MODE>
+// ---------------------------------------------------------------------------
+// proto4z framing of decrypted session buffers:
+// TcpSession::onRecv's loop (src/frame/session.cpp:329-371) over HasRawPacket
+// (depends/proto4z/proto4z.h:704-748): walk from the buffer start, one packet
+// per check, until shortage (status 1) or corruption (status 2).  One lane per
+// session: a chain of dependent header reads (4 byte loads each, headers sit
+// at any alignment).  Bytes past the last header read are never touched.
+// Used standalone (frame_scan_kernel) and fused into crypt_kernel's epilogue
+// (FRAME = true: each lane frames its own session right after decrypting it,
+// no second launch).
+// ---------------------------------------------------------------------------
+struct FrameArgs {
+    const uint64_t *off;   // buffer of entry e = payload + off[e] ...
+    const uint32_t *len;   // ... len[e] bytes (the whole receive block, not just the decrypted tail)
+    uint32_t bound, maxp;
+    uint32_t *npk, *used, *status, *pkt_len;
+};
+
+__device__ __forceinline__ uint32_t load_le32(const uint8_t *p)
+{
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__device__ __forceinline__ void frame_walk(const uint8_t *b, uint32_t L, uint32_t bound, uint32_t maxp, uint32_t e,
+                                           uint32_t *npk, uint32_t *used, uint32_t *status, uint32_t *pkt_len)
+{
+    const uint32_t headLen = 4u + 2u;          // sizeof(LenInteger) + sizeof(ProtoInteger), proto4z.h:714
+    uint32_t u = 0, k = 0, st;
+    for (;;) {
+        const uint32_t cur = L - u, bl = bound - u;
+        if (bl < cur || bound < bl) { st = 2u; break; }              // :708-711
+        if (cur < headLen) { st = 1u; break; }                       // :715-718
+        const uint32_t pl = load_le32(b + u);                        // ReadPodData, :717
+        if (pl < headLen) { st = 2u; break; }                        // :718-721
+        if (pl > bl) { st = pl > bound ? 2u : 1u; break; }          // :722-732
+        if (pl > bound) { st = 2u; break; }                          // :735-738
+        if (pl > cur) { st = 1u; break; }                            // :747
+        if (pkt_len && k < maxp) pkt_len[(size_t)e * maxp + k] = pl;
+        ++k;
+        u += pl;
+    }
+    npk[e] = k;
+    used[e] = u;
+    status[e] = st;
+}
+
+template <int MODE, bool FRAME = false>
 __global__ void __launch_bounds__(256, 2)
 crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
              const uint32_t *__restrict__ ids, uint32_t first_slot,
              uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
              const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
-             uint32_t *__restrict__ err, uint8_t *__restrict__ sink)
+             uint32_t *__restrict__ err, uint8_t *__restrict__ sink, FrameArgs fr = FrameArgs{})
 {
     // one LDS object: the 64 KiB S-box image, then 16 B of workgroup flags
     __shared__ __attribute__((aligned(16))) uint8_t smem[kGroupBytes + 16];
@@ -727,7 +773,13 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         __syncthreads();
         const uint32_t gmin = flag[0], gmax = flag[1];
         __syncthreads();
-        if (gmin == 0xFFFFFFFFu) return;                  // an idle bucket
+        if (gmin == 0xFFFFFFFFu) {                        // an idle bucket: nothing to decrypt
+            if constexpr (FRAME) {
+                if (valid) frame_walk(payload + fr.off[e], fr.len[e], fr.bound, fr.maxp, e, fr.npk, fr.used,
+                                      fr.status, fr.pkt_len);
+            }
+            return;
+        }
         if (gmin != gmax) {
             if (j == 0) latch_fault(err, kErrGroup);
             return;
@@ -783,6 +835,15 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         lane_init(st, S, col, sxy);
         crypt_message(S, st, msg, mylen, A, pre);
         xy[slot] = lane_xy(st);
+    }
+    if constexpr (FRAME) {
+        // The lane's own decrypted bytes: its stores must have landed before
+        // it reads the headers back.
+        if (valid) {
+            __builtin_amdgcn_s_waitcnt(0);
+            frame_walk(payload + fr.off[e], fr.len[e], fr.bound, fr.maxp, e, fr.npk, fr.used, fr.status,
+                       fr.pkt_len);
+        }
     }
     stamp(ts, 2);
 
@@ -1304,21 +1365,8 @@ xor_ring_kernel(uint8_t *__restrict__ ring, uint32_t cap, const uint32_t *__rest
     }
 }
 
-// ---------------------------------------------------------------------------
-// frame_scan_kernel: proto4z framing of decrypted session buffers, device
-// side.  TcpSession::onRecv's loop
-// (src/frame/session.cpp:329-371) over HasRawPacket
-// (depends/proto4z/proto4z.h:704-748): walk from the buffer start, one packet
-// per check, until shortage (status 1) or corruption (status 2).  One lane per
-// session: the walk is a chain of dependent header reads (4 byte loads each,
-// headers sit at any alignment), so lanes run independent sessions side by
-// side.  Bytes past the last header read are never touched.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t load_le32(const uint8_t *p)
-{
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-
+// frame_scan_kernel: the framing walk (frame_walk) as its own launch over
+// already-decrypted, device-resident buffers (zrc4_frame_scan).
 __global__ void __launch_bounds__(256)
 frame_scan_kernel(const uint8_t *__restrict__ buf, const uint64_t *__restrict__ off,
                   const uint32_t *__restrict__ len, uint32_t bound, uint32_t n, uint32_t maxp,
@@ -1327,26 +1375,7 @@ frame_scan_kernel(const uint8_t *__restrict__ buf, const uint64_t *__restrict__ 
 {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
-    const uint8_t *b = buf + off[e];
-    const uint32_t L = len[e];
-    const uint32_t headLen = 4u + 2u;          // sizeof(LenInteger) + sizeof(ProtoInteger), proto4z.h:714
-    uint32_t u = 0, k = 0, st;
-    for (;;) {
-        const uint32_t cur = L - u, bl = bound - u;
-        if (bl < cur || bound < bl) { st = 2u; break; }              // :708-711
-        if (cur < headLen) { st = 1u; break; }                       // :715-718
-        const uint32_t pl = load_le32(b + u);                        // ReadPodData, :717
-        if (pl < headLen) { st = 2u; break; }                        // :718-721
-        if (pl > bl) { st = pl > bound ? 2u : 1u; break; }          // :722-732
-        if (pl > bound) { st = 2u; break; }                          // :735-738
-        if (pl > cur) { st = 1u; break; }                            // :747
-        if (pkt_len && k < maxp) pkt_len[(size_t)e * maxp + k] = pl;
-        ++k;
-        u += pl;
-    }
-    npk[e] = k;
-    used[e] = u;
-    status[e] = st;
+    frame_walk(buf + off[e], len[e], bound, maxp, e, npk, used, status, pkt_len);
 }
 
 // identity_kernel: every slot of every group gets the identity S-box (row k of

@@ -596,15 +596,23 @@ void SessionManager::onWritable(const TcpSessionPtr &sp)
     }
 }
 
-void SessionManager::dispatchRecv(const TcpSessionPtr &sp)
+void SessionManager::dispatchRecv(const TcpSessionPtr &sp, const Rc4Frame *fr)
 {
     // session.cpp:326-467 (PT_TCP): frame and dispatch the decrypted bytes.
+    // With `fr` the device already ran the check loop over this block (fused
+    // into the decrypt launch): its first packets are taken from there, and
+    // the host check resumes where the device list ends (it then reports the
+    // same shortage / corruption the device stopped on).
     TcpSession &s = *sp;
     SessionBlock *rb = s._recving;
     unsigned int used = 0;
+    uint32_t k = 0;
+    const uint32_t pre = fr ? std::min(fr->npk, Rc4Frame::kMaxPackets) : 0u;
     while (!s._closing && s._status == 2) {
         RawPacketCheckResult ret;
-        try {
+        if (k < pre) {
+            ret = RawPacketCheckResult(BCT_SUCCESS, fr->pkt[k++]);
+        } else try {
             ret = s._options._onRawPacketCheck(rb->begin + used, rb->len - used, rb->bound - used, rb->bound);
         } catch (...) {
             s.close();
@@ -662,21 +670,38 @@ void SessionManager::flushHooks()
 
     // One crypt for the whole iteration.
     _spans.clear();
-    for (TcpSessionPtr &sp : _recvBatch) {
-        TcpSession &s = *sp;
+    _frames.clear();
+    _recvFrame.assign(_recvBatch.size(), -1);
+    const bool devFrame = _deviceFraming && _rc4 && _rc4->canFrame();
+    typedef RawPacketCheckResult (*CheckFn)(const char *, unsigned int, unsigned int, unsigned int);
+    for (size_t r = 0; r < _recvBatch.size(); ++r) {
+        TcpSession &s = *_recvBatch[r];
         if (s._options._rc4TcpEncryption.empty() || s._recvFresh == 0 || s._recving->len == 0) continue;
         // session.cpp:315-323: the freshly received tail
         const unsigned int n = s._recvFresh < s._recving->len ? s._recvFresh : s._recving->len;
         _spans.push_back({s._slotRead, n, reinterpret_cast<uint8_t *>(s._recving->begin + s._recving->len - n)});
+        if (devFrame) {
+            Rc4Frame f;
+            const CheckFn *fn = s._options._onRawPacketCheck.target<CheckFn>();
+            if (fn && *fn == &DefaultRawPacketCheck && s._recving->bound == SESSION_BLOCK_SIZE) {
+                f.block = reinterpret_cast<const uint8_t *>(s._recving->begin);
+                f.len = s._recving->len;
+                _recvFrame[r] = (int)_frames.size();
+            }
+            _frames.push_back(f);
+        }
     }
     for (TcpSessionPtr &sp : _sendBatch) {
         TcpSession &s = *sp;
         if (s._options._rc4TcpEncryption.empty()) continue;
         _spans.push_back({s._slotWrite, s._sending->len, reinterpret_cast<uint8_t *>(s._sending->begin)});
+        if (devFrame) _frames.emplace_back();
     }
     if (!_spans.empty()) {
         const auto t0 = std::chrono::steady_clock::now();
-        const int rc = hooks()->crypt(_spans.data(), (uint32_t)_spans.size());
+        const int rc = devFrame ? hooks()->cryptFrame(_spans.data(), (uint32_t)_spans.size(), _frames.data(),
+                                                      SESSION_BLOCK_SIZE)
+                                : hooks()->crypt(_spans.data(), (uint32_t)_spans.size());
         const auto t1 = std::chrono::steady_clock::now();
         _statInfo[STAT_RC4_CALLS]++;
         _statInfo[STAT_RC4_SPANS] += _spans.size();
@@ -703,9 +728,13 @@ void SessionManager::flushHooks()
         writeSending(sp);
     }
     _sendBatch.clear();
-    for (TcpSessionPtr &sp : _recvBatch) {
+    for (size_t r = 0; r < _recvBatch.size(); ++r) {
+        TcpSessionPtr &sp = _recvBatch[r];
         sp->_recvFresh = 0;
-        if (!sp->_closing) dispatchRecv(sp);
+        if (sp->_closing) continue;
+        const int fi = _recvFrame.empty() ? -1 : _recvFrame[r];
+        if (fi >= 0) _statInfo[STAT_RC4_FRAMED]++;
+        dispatchRecv(sp, fi >= 0 ? &_frames[(size_t)fi] : nullptr);
     }
     _recvBatch.clear();
 }

@@ -6,31 +6,43 @@
 // in place -- no staging copies and no per-session calls.  The batch tables
 // (slot ids, offsets, lengths, keys) are pinned too.  Payload addressing:
 // kernels take one base pointer and 64-bit per-entry offsets; the base is the
-// first slab and an entry's offset is its address minus the base in two's
-// complement, so slabs anywhere in the address space share one launch.
+// first pinned allocation and an entry's offset is its address minus the base
+// in two's complement, so slabs anywhere in the address space share one launch.
+//
+// Every launch is a zrc4_crypt_grouped batch: entries sorted by slot, one
+// 256-entry bucket per 256-slot group touched, so each bucket moves its
+// group's S-boxes as one coalesced 64 KiB image whatever subset of the group
+// the iteration touches (the kIds gather path is never used here).
 //
 // Two modes:
-//   direct     one zrc4_crypt per engine iteration over the spans themselves.
-//              A span's latency is its serial RC4 chain: ~40 us per KiB on one
-//              lane (rc4_encryption.h:83-88 is byte-serial), so small batches
-//              wait on the chain.
+//   direct     one grouped launch per engine iteration over the spans
+//              themselves, then a wait.  A span's latency is its serial RC4
+//              chain: ~40 ns per byte on one lane (rc4_encryption.h:83-88 is
+//              byte-serial), so small batches wait on the chain.
 //   reservoir  (default) RC4's keystream does not depend on the data, so each
-//              slot's keystream is generated AHEAD into a device ring of
-//              `ring` bytes (HBM; 32 KiB x 2 slots per session) on a background
-//              stream, and an iteration's hook is one zrc4_xor_ring launch --
-//              data-parallel, no chain on the latency path.  A slot whose ring
-//              runs short is topped up synchronously (exactly the missing bytes)
-//              before the XOR.  Keystream bytes are consumed strictly in order,
-//              so the wire bytes are unchanged.
-// Ordering rules (streams: A = hook calls, B = background refill):
-//   * the consumer reads only ring bytes of COMMITTED refills (their event has
-//     completed); a refill writes only ring bytes already consumed (zeroed by a
-//     completed consumer) -- the two never touch the same bytes;
-//   * kernels that touch slot state (ksa, top-up, refill) never run on A and B
-//     at once: A waits for B before a seed or a top-up.
+//              slot's keystream is generated AHEAD by the GPU -- a background
+//              stream runs zrc4_crypt over the slot's ring bytes (kept zero:
+//              0 ^ k = k) -- into a ring of `ring` bytes in PINNED HOST memory
+//              (written over PCIe by the kernel).  The hook then XORs each
+//              span with committed ring bytes on the host: no GPU round trip
+//              on the latency path.  Only a slot whose committed keystream
+//              does not cover its span goes to the GPU synchronously, and only
+//              for the missing tail (the slot's state sits exactly at the end
+//              of its committed keystream).  The RC4 state never leaves the
+//              device; keystream bytes are consumed strictly in order, so the
+//              wire bytes are the reference's.
+// Ordering rules (streams: A = synchronous work, B = background refill):
+//   * the host reads only ring bytes of COMMITTED refills (their event has
+//     completed), and zeroes them as it consumes them; a refill writes only
+//     ring bytes past the committed end -- the two never touch the same bytes;
+//   * kernels that touch slot state (ksa, tail crypt, refill) never run on A
+//     and B at once: a grouped kernel stores its whole group image, so A
+//     waits for every queued refill on B before a seed or a tail crypt;
+//   * refills on B run in stream order, at most kRefillDepth queued.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -69,33 +81,107 @@ struct PinnedArray {
     }
 };
 
-// One batch table (ids / offsets / lengths / ring positions) in pinned memory.
+// One grouped batch table (ids / offsets / lengths) in pinned memory.
 struct Table {
-    PinnedArray<uint32_t> ids, len, pos;
+    PinnedArray<uint32_t> ids, len;
     PinnedArray<uint64_t> off;
     uint32_t n = 0;
     void clear() { n = 0; }
-    void push(uint32_t id, uint64_t o, uint32_t l, uint32_t p = 0)
+    void push(uint32_t id, uint64_t o, uint32_t l)
     {
-        if (n == ids.cap || n == off.cap || n == len.cap || n == pos.cap) {
+        if (n == ids.cap || n == off.cap || n == len.cap) {
             ids.reserve(n + 1);
             off.reserve(n + 1);
             len.reserve(n + 1);
-            pos.reserve(n + 1);
         }
         ids.p[n] = id;
         off.p[n] = o;
         len.p[n] = l;
-        pos.p[n] = p;
         ++n;
     }
 };
 
-struct Level {
-    uint64_t gen = 0;    // keystream bytes generated and committed
-    uint64_t use = 0;    // keystream bytes consumed
-    uint64_t pend = 0;   // generated by the in-flight refill (valid while it runs)
+struct Entry {
+    uint32_t slot;
+    uint32_t len;
+    uint64_t off;
+    uint32_t idx = 0;     // the caller's span index (framed calls)
+    uint32_t flen = 0;    // frame block length (framed calls)
+    uint64_t foff = 0;    // frame block offset from the base (framed calls)
 };
+
+// Per-entry framing tables of a framed grouped launch (pinned).
+struct FrameTable {
+    PinnedArray<uint64_t> off;
+    PinnedArray<uint32_t> len, npk, used, status, pkt;
+    std::vector<int64_t> idx;   // batch entry -> span index (-1: padding)
+    void reserve(size_t n)
+    {
+        off.reserve(n);
+        len.reserve(n);
+        npk.reserve(n);
+        used.reserve(n);
+        status.reserve(n);
+        pkt.reserve(n * Rc4Frame::kMaxPackets);
+    }
+};
+
+// zrc4_crypt_grouped layout: entries sorted by slot, a new 256-entry bucket
+// at every group change (each group holds at most 256 distinct slots, so one
+// bucket per group).
+void buildGrouped(Table &t, std::vector<Entry> &es, FrameTable *ft = nullptr)
+{
+    std::sort(es.begin(), es.end(), [](const Entry &a, const Entry &b) { return a.slot < b.slot; });
+    t.clear();
+    if (ft) ft->idx.clear();
+    auto push = [&](uint32_t slot, uint64_t off, uint32_t len, const Entry *e) {
+        t.push(slot, off, len);
+        if (ft) {
+            ft->reserve(t.n);
+            ft->off.p[t.n - 1] = e ? e->foff : 0;
+            ft->len.p[t.n - 1] = e ? e->flen : 0;
+            ft->idx.push_back(e ? (int64_t)e->idx : -1);
+        }
+    };
+    uint32_t cur = ZRC4_IDLE_SLOT;
+    for (const Entry &e : es) {
+        const uint32_t g = e.slot >> 8;
+        if (g != cur) {
+            while (t.n % ZRC4_GROUP_SLOTS) push(ZRC4_IDLE_SLOT, 0, 0, nullptr);
+            cur = g;
+        }
+        push(e.slot, e.off, e.len, &e);
+    }
+}
+
+struct Level {
+    uint64_t gen = 0;    // keystream bytes generated and committed (absolute stream position)
+    uint64_t use = 0;    // keystream bytes consumed
+    uint64_t pend = 0;   // end of the last queued refill (== gen when none is in flight)
+};
+
+// One background refill launch: its grouped table, its completion event and
+// the (slot, end position) pairs it commits.
+struct Refill {
+    Table t;
+    hipEvent_t ev = nullptr;
+    std::vector<std::pair<uint32_t, uint64_t>> ends;
+};
+
+// dst ^= src for n bytes, then src = 0 (word-wise where possible).
+void xorAndClear(uint8_t *__restrict dst, uint8_t *__restrict src, size_t n)
+{
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t a, b;
+        std::memcpy(&a, dst + i, 8);
+        std::memcpy(&b, src + i, 8);
+        a ^= b;
+        std::memcpy(dst + i, &a, 8);
+    }
+    for (; i < n; ++i) dst[i] ^= src[i];
+    std::memset(src, 0, n);
+}
 
 class DeviceRc4Hooks final : public Rc4Hooks {
 public:
@@ -106,17 +192,18 @@ public:
             throw std::runtime_error(std::string("makeDeviceRc4Hooks: zrc4_create: ") + zrc4_strerror(rc));
         bool ok = hipSetDevice(device) == hipSuccess &&
                   hipStreamCreateWithFlags(&sA_, hipStreamNonBlocking) == hipSuccess &&
-                  hipStreamCreateWithFlags(&sB_, hipStreamNonBlocking) == hipSuccess &&
-                  hipEventCreateWithFlags(&evB_, hipEventDisableTiming) == hipSuccess;
-        if (ok && ringCap_) {
-            const size_t bytes = (size_t)zrc4_capacity(ctx_) * ringCap_;
-            ok = hipMalloc(&ring_, bytes) == hipSuccess && hipMemsetAsync(ring_, 0, bytes, sA_) == hipSuccess &&
-                 hipStreamSynchronize(sA_) == hipSuccess;
-            level_.resize(zrc4_capacity(ctx_));
-        }
+                  hipStreamCreateWithFlags(&sB_, hipStreamNonBlocking) == hipSuccess;
+        for (Refill &r : refill_) ok = ok && hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) == hipSuccess;
         if (!ok) {
             release();
-            throw std::runtime_error("makeDeviceRc4Hooks: HIP stream/event/ring allocation failed");
+            throw std::runtime_error("makeDeviceRc4Hooks: HIP stream/event creation failed");
+        }
+        seen_.assign(zrc4_capacity(ctx_), 0u);
+        if (ringCap_) {
+            level_.resize(zrc4_capacity(ctx_));
+            ringSlab_.assign(zrc4_capacity(ctx_) / ZRC4_GROUP_SLOTS, nullptr);
+            hungryMark_.assign(zrc4_capacity(ctx_), 0u);
+            refillChunk_ = std::max<uint32_t>(256u, std::min<uint32_t>(kRefillChunk, ringCap_ / 4));
         }
     }
     ~DeviceRc4Hooks() override { release(); }
@@ -143,6 +230,7 @@ public:
         const uint64_t ko = keyBytes_.size();
         keyBytes_.insert(keyBytes_.end(), key.data(), key.data() + kl);
         for (uint32_t i = 0; i < n; ++i) {
+            if (slots[i] >= capacity()) return ZRC4_ERR_SLOT_RANGE;
             seedIds_.push_back(slots[i]);
             seedOff_.push_back(ko);
             seedLen_.push_back(kl);
@@ -155,151 +243,291 @@ public:
         int rc = flushSeeds();
         if (rc != ZRC4_OK) return rc;
         if (n == 0) return ZRC4_OK;
-        if (!base_) return ZRC4_ERR_INVALID_ARG;
-        if (ringCap_)
-            for (uint32_t i = 0; i < n; ++i)
-                if (spans[i].len > ringCap_) return ZRC4_ERR_INVALID_ARG;
+        // Each slot at most once per call (rc4_hooks.h contract): a second span
+        // of one slot would consume keystream the first already accounted for.
+        if (++callStamp_ == 0) {
+            std::fill(seen_.begin(), seen_.end(), 0u);
+            callStamp_ = 1;
+        }
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t s = spans[i].slot;
+            if (s >= seen_.size() || seen_[s] == callStamp_) return ZRC4_ERR_INVALID_ARG;
+            seen_[s] = callStamp_;
+        }
         return ringCap_ ? cryptReservoir(spans, n) : cryptDirect(spans, n);
     }
 
+    // Device framing rides on the direct mode's launch (the reservoir mode
+    // decrypts on the host, so there is no device pass to fuse with).
+    bool canFrame() const override { return ringCap_ == 0; }
+
+    int cryptFrame(const Rc4Span *spans, uint32_t n, Rc4Frame *frames, uint32_t bound) override
+    {
+        if (ringCap_) return ZRC4_ERR_INVALID_ARG;
+        int rc = flushSeeds();
+        if (rc != ZRC4_OK) return rc;
+        if (n == 0) return ZRC4_OK;
+        if (++callStamp_ == 0) {
+            std::fill(seen_.begin(), seen_.end(), 0u);
+            callStamp_ = 1;
+        }
+        es_.clear();
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t s = spans[i].slot;
+            if (s >= seen_.size() || seen_[s] == callStamp_) return ZRC4_ERR_INVALID_ARG;
+            seen_[s] = callStamp_;
+            Entry e{s, spans[i].len, offOf(spans[i].data)};
+            e.idx = i;
+            e.flen = frames[i].len;
+            e.foff = frames[i].len ? offOf(frames[i].block) : 0;
+            es_.push_back(e);
+            tailBytes_ += spans[i].len;
+        }
+        buildGrouped(tt_, es_, &ft_);
+        zrc4_frame_args fa{ft_.off.p, ft_.len.p, bound, Rc4Frame::kMaxPackets, ft_.npk.p, ft_.used.p,
+                           ft_.status.p, ft_.pkt.p};
+        rc = zrc4_crypt_grouped_frame(ctx_, tt_.ids.p, base_, tt_.off.p, tt_.len.p, tt_.n, &fa, sA_);
+        if (rc != ZRC4_OK) return rc;
+        ++tailLaunches_;
+        if ((rc = zrc4_sync(ctx_, sA_)) != ZRC4_OK) return rc;
+        for (uint32_t b = 0; b < tt_.n; ++b) {
+            const int64_t i = ft_.idx[b];
+            if (i < 0 || !frames[i].len) continue;
+            Rc4Frame &f = frames[i];
+            f.npk = ft_.npk.p[b];
+            f.used = ft_.used.p[b];
+            f.status = ft_.status.p[b];
+            const uint32_t k = std::min(f.npk, Rc4Frame::kMaxPackets);
+            std::memcpy(f.pkt, ft_.pkt.p + (size_t)b * Rc4Frame::kMaxPackets, k * sizeof(uint32_t));
+            ++framed_;
+        }
+        return ZRC4_OK;
+    }
+
+    std::string stats() const override
+    {
+        char b[512];
+        std::snprintf(b, sizeof b,
+                      "{\"ring_bytes\": %llu, \"tail_bytes\": %llu, \"tail_launches\": %llu, "
+                      "\"refill_bytes\": %llu, \"refill_launches\": %llu, \"refill_waits\": %llu, "
+                      "\"ring_cap\": %u, \"refill_chunk\": %u, \"device_framed\": %llu}",
+                      ringBytes_, tailBytes_, tailLaunches_, refillBytes_, refillLaunches_, refillWaits_, ringCap_,
+                      refillChunk_, framed_);
+        return b;
+    }
+
 private:
-    uint64_t offOf(const void *p) const { return (uint64_t)((uintptr_t)p - (uintptr_t)base_); }
+    uint64_t offOf(const void *p)
+    {
+        if (!base_) base_ = static_cast<uint8_t *>(const_cast<void *>(p));
+        return (uint64_t)((uintptr_t)p - (uintptr_t)base_);
+    }
+
+    // The ring of slot s: pinned host memory, one slab of 256 rings per group,
+    // allocated on first use and zeroed (the zero invariant of the refills).
+    uint8_t *ringOf(uint32_t s)
+    {
+        uint8_t *&slab = ringSlab_[s / ZRC4_GROUP_SLOTS];
+        if (!slab) {
+            const size_t bytes = (size_t)ZRC4_GROUP_SLOTS * ringCap_;
+            void *p = nullptr;
+            if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+            std::memset(p, 0, bytes);
+            slab = static_cast<uint8_t *>(p);
+        }
+        return slab + (size_t)(s % ZRC4_GROUP_SLOTS) * ringCap_;
+    }
+
+    // One grouped launch on A over `es`, then the wait.
+    int runTail(std::vector<Entry> &es)
+    {
+        if (es.empty()) return ZRC4_OK;
+        buildGrouped(tt_, es);
+        int rc = zrc4_crypt_grouped(ctx_, tt_.ids.p, base_, tt_.off.p, tt_.len.p, tt_.n, sA_);
+        if (rc != ZRC4_OK) return rc;
+        ++tailLaunches_;
+        return zrc4_sync(ctx_, sA_);
+    }
 
     int cryptDirect(const Rc4Span *spans, uint32_t n)
     {
-        tc_.clear();
-        for (uint32_t i = 0; i < n; ++i) tc_.push(spans[i].slot, offOf(spans[i].data), spans[i].len);
-        int rc = zrc4_crypt(ctx_, tc_.ids.p, base_, tc_.off.p, tc_.len.p, n, sA_);
-        return rc != ZRC4_OK ? rc : zrc4_sync(ctx_, sA_);
+        es_.clear();
+        for (uint32_t i = 0; i < n; ++i)
+            if (spans[i].len) es_.push_back({spans[i].slot, spans[i].len, offOf(spans[i].data)});
+        for (const Entry &e : es_) tailBytes_ += e.len;
+        return runTail(es_);
     }
 
     int cryptReservoir(const Rc4Span *spans, uint32_t n)
     {
-        int rc = pollRefill(false);
+        int rc = pollRefills(false);
         if (rc != ZRC4_OK) return rc;
-        // Slots whose committed keystream does not cover their span.
-        bool shortAny = false;
-        for (uint32_t i = 0; i < n; ++i) {
-            const Level &L = level_[spans[i].slot];
-            if (L.gen - L.use < spans[i].len) shortAny = true;
+        // A slot short of committed keystream while refills are queued: wait
+        // for them in order until it is covered or none is left (their bytes
+        // are the ones it needs, and a tail crypt may not run beside them).
+        for (;;) {
+            bool wait = false;
+            for (uint32_t i = 0; i < n && !wait; ++i) {
+                const Level &L = level_[spans[i].slot];
+                if (L.gen - L.use < spans[i].len && L.pend > L.gen) wait = true;
+            }
+            if (!wait) break;
+            ++refillWaits_;
+            if ((rc = commitOldest(true)) != ZRC4_OK) return rc;
         }
-        if (shortAny) {
-            if ((rc = pollRefill(true)) != ZRC4_OK) return rc;   // slot state must be quiet
-            // Top up exactly the missing bytes on A (at most two pieces per slot:
-            // up to the ring end, then from its start).
-            // Each piece has its own pinned table: piece 1 is filled while piece
-            // 0's kernel may still be reading its table.
-            for (int piece = 0; piece < 2; ++piece) {
-                Table &tt_ = tp_[piece];
-                tt_.clear();
-                for (uint32_t i = 0; i < n; ++i) {
-                    Level &L = level_[spans[i].slot];
-                    const uint64_t need = L.use + spans[i].len;
-                    if (L.gen >= need) continue;
-                    const uint32_t at = (uint32_t)(L.gen % ringCap_);
-                    const uint32_t amt = (uint32_t)std::min<uint64_t>(need - L.gen, ringCap_ - at);
-                    tt_.push(spans[i].slot, (uint64_t)spans[i].slot * ringCap_ + at, amt);
-                    L.gen += amt;
+        // Host XOR with the committed ring bytes; collect the uncovered tails.
+        es_.clear();
+        for (uint32_t i = 0; i < n; ++i) {
+            const Rc4Span &sp = spans[i];
+            if (!sp.len) continue;
+            Level &L = level_[sp.slot];
+            const uint32_t have = (uint32_t)std::min<uint64_t>(L.gen - L.use, sp.len);
+            if (have) {
+                uint8_t *r = ringOf(sp.slot);
+                uint32_t done = 0;
+                while (done < have) {
+                    const uint32_t at = (uint32_t)((L.use + done) % ringCap_);
+                    const uint32_t k = std::min(have - done, ringCap_ - at);
+                    xorAndClear(sp.data + done, r + at, k);
+                    done += k;
                 }
-                if (tt_.n == 0) break;
-                rc = zrc4_crypt(ctx_, tt_.ids.p, ring_, tt_.off.p, tt_.len.p, tt_.n, sA_);
-                if (rc != ZRC4_OK) return rc;
+                L.use += have;
+                ringBytes_ += have;
+            }
+            if (have < sp.len) {
+                // the slot's device state is at position L.gen == L.use
+                es_.push_back({sp.slot, sp.len - have, offOf(sp.data + have)});
+                L.use += sp.len - have;
+                L.gen = L.pend = L.use;
+                tailBytes_ += sp.len - have;
+            }
+            if (!hungryMark_[sp.slot]) {
+                hungryMark_[sp.slot] = 1;
+                hungry_.push_back(sp.slot);
             }
         }
-        tc_.clear();
-        for (uint32_t i = 0; i < n; ++i) {
-            Level &L = level_[spans[i].slot];
-            tc_.push(spans[i].slot, offOf(spans[i].data), spans[i].len, (uint32_t)(L.use % ringCap_));
-            L.use += spans[i].len;
+        if (!es_.empty()) {
+            if ((rc = drainRefills()) != ZRC4_OK) return rc;     // slot state must be quiet
+            if ((rc = runTail(es_)) != ZRC4_OK) return rc;
         }
-        rc = zrc4_xor_ring(ctx_, ring_, ringCap_, tc_.ids.p, tc_.pos.p, base_, tc_.off.p, tc_.len.p, tc_.n, sA_);
-        if (rc != ZRC4_OK) return rc;
-        rc = zrc4_sync(ctx_, sA_);
-        if (rc != ZRC4_OK) return rc;
-        return launchRefill(spans, n);
-    }
-
-    // Background refill of the slots just used, up to a full ring, in chunks
-    // of at most kRefillChunk bytes (one chunk's chain ~ kRefillChunk x 40 ns).
-    int launchRefill(const Rc4Span *spans, uint32_t n)
-    {
-        if (refillInFlight_ || debugNoRefill_) return ZRC4_OK;
-        tr_.clear();
-        refillSlots_.clear();
-        for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t s = spans[i].slot;
-            Level &L = level_[s];
-            const uint64_t level = L.gen - L.use;
-            if (level * 2 >= ringCap_ || L.pend > L.gen) continue;   // at least half full, or already queued
-            const uint32_t at = (uint32_t)(L.gen % ringCap_);
-            const uint32_t amt = (uint32_t)std::min<uint64_t>(
-                std::min<uint64_t>(ringCap_ - level, ringCap_ - at), kRefillChunk);
-            tr_.push(s, (uint64_t)s * ringCap_ + at, amt);
-            L.pend = L.gen + amt;
-            refillSlots_.push_back(s);
+        while (inFlight_ < kRefillDepth) {
+            const uint32_t before = inFlight_;
+            if ((rc = launchRefill()) != ZRC4_OK) return rc;
+            if (inFlight_ == before) break;
         }
-        if (tr_.n == 0) return ZRC4_OK;
-        int rc = zrc4_crypt(ctx_, tr_.ids.p, ring_, tr_.off.p, tr_.len.p, tr_.n, sB_);
-        if (rc != ZRC4_OK) return rc;
-        if (hipEventRecord(evB_, sB_) != hipSuccess) return ZRC4_ERR_HIP;
-        refillInFlight_ = true;
-        if (debugSyncRefill_) return pollRefill(true);
         return ZRC4_OK;
     }
 
-    // Commit the in-flight refill if it has finished (wait = block until it has).
-    int pollRefill(bool wait)
+    // Background refill of the slots used since the last one, each up to a
+    // full ring (counting what is already queued), in one piece of at most
+    // refillChunk_ bytes per slot (one chunk's chain ~ refillChunk_ x 40 ns),
+    // written straight into the pinned host rings.  Up to kRefillDepth
+    // refills are queued back to back on stream B, so a stream's keystream
+    // generation does not pause between launches (stream order keeps each
+    // slot's pieces sequential).
+    int launchRefill()
     {
-        if (!refillInFlight_) return ZRC4_OK;
+        if (inFlight_ >= kRefillDepth || debugNoRefill_ || hungry_.empty()) return ZRC4_OK;
+        Refill &R = refill_[(head_ + inFlight_) % kRefillDepth];
+        rs_.clear();
+        R.ends.clear();
+        std::vector<uint32_t> keep;
+        for (uint32_t s : hungry_) {
+            Level &L = level_[s];
+            const uint64_t level = L.pend - L.use;
+            // Whole chunks only: a launch lasts as long as its longest piece
+            // (one lane per slot), so every slot it carries gets a full chunk
+            // (or the piece up to the ring end).  A slot without room for one
+            // leaves the hungry list until it is consumed from again.
+            if (ringCap_ - level < refillChunk_) {
+                hungryMark_[s] = 0;
+                continue;
+            }
+            const uint32_t at = (uint32_t)(L.pend % ringCap_);
+            const uint32_t amt = std::min(ringCap_ - at, refillChunk_);
+            rs_.push_back({s, amt, offOf(ringOf(s) + at)});
+            L.pend += amt;
+            R.ends.push_back({s, L.pend});
+            keep.push_back(s);                      // re-examined at the next launch
+        }
+        hungry_.swap(keep);
+        if (rs_.empty()) return ZRC4_OK;
+        buildGrouped(R.t, rs_);
+        int rc = zrc4_crypt_grouped(ctx_, R.t.ids.p, base_, R.t.off.p, R.t.len.p, R.t.n, sB_);
+        if (rc != ZRC4_OK) return rc;
+        if (hipEventRecord(R.ev, sB_) != hipSuccess) return ZRC4_ERR_HIP;
+        ++inFlight_;
+        ++refillLaunches_;
+        if (debugSyncRefill_) return drainRefills();
+        return ZRC4_OK;
+    }
+
+    // Commit the oldest queued refill if it has finished (wait = block until
+    // it has).  Refills complete in stream order.
+    int commitOldest(bool wait)
+    {
+        if (!inFlight_) return ZRC4_OK;
+        Refill &R = refill_[head_];
         if (wait) {
-            int rc = zrc4_sync(ctx_, sB_);
-            if (rc != ZRC4_OK) return rc;
+            if (hipEventSynchronize(R.ev) != hipSuccess) return ZRC4_ERR_HIP;
         } else {
-            const hipError_t q = hipEventQuery(evB_);
-            if (q == hipErrorNotReady) return ZRC4_OK;
+            const hipError_t q = hipEventQuery(R.ev);
+            if (q == hipErrorNotReady) return ZRC4_ERR_NOT_READY_;
             if (q != hipSuccess) return ZRC4_ERR_HIP;
         }
-        for (uint32_t s : refillSlots_) {
-            Level &L = level_[s];
-            if (L.pend > L.gen) L.gen = L.pend;
+        for (const auto &se : R.ends) {
+            Level &L = level_[se.first];
+            if (se.second > L.gen) {
+                refillBytes_ += se.second - L.gen;
+                L.gen = se.second;
+            }
         }
-        refillSlots_.clear();
-        refillInFlight_ = false;
+        R.ends.clear();
+        head_ = (head_ + 1) % kRefillDepth;
+        --inFlight_;
         return ZRC4_OK;
     }
 
+    // Commit every finished refill (wait = every queued one), then report
+    // latched device faults of stream B.
+    int pollRefills(bool wait)
+    {
+        bool any = false;
+        while (inFlight_) {
+            const int rc = commitOldest(wait);
+            if (rc == ZRC4_ERR_NOT_READY_) break;
+            if (rc != ZRC4_OK) return rc;
+            any = true;
+        }
+        return any ? zrc4_sync(ctx_, sB_) : ZRC4_OK;
+    }
+    int drainRefills() { return pollRefills(true); }
+
     // Queued makeSBox calls: one zrc4_ksa ahead of the hook work on A.  In
-    // reservoir mode a reseeded slot's unconsumed keystream is first drained
-    // (XORed into scratch, which zeroes the ring) and its counters restart.
+    // reservoir mode a reseeded slot's unconsumed keystream is dropped (its
+    // ring bytes zeroed on the host) and its counters restart.
     int flushSeeds()
     {
         const uint32_t m = (uint32_t)seedIds_.size();
         if (m == 0) return ZRC4_OK;
         int rc;
         if (ringCap_) {
-            if ((rc = pollRefill(true)) != ZRC4_OK) return rc;
-            tt_.clear();
-            uint32_t maxLeft = 0;
+            if ((rc = drainRefills()) != ZRC4_OK) return rc;
             for (uint32_t s : seedIds_) {
                 Level &L = level_[s];
-                const uint32_t left = (uint32_t)(L.gen - L.use);
-                if (left) {
-                    tt_.push(s, 0, left, (uint32_t)(L.use % ringCap_));
-                    maxLeft = std::max(maxLeft, left);
+                if (L.gen > L.use) {
+                    uint8_t *r = ringOf(s);
+                    for (uint64_t p = L.use; p < L.gen;) {
+                        const uint32_t at = (uint32_t)(p % ringCap_);
+                        const uint32_t k = (uint32_t)std::min<uint64_t>(L.gen - p, ringCap_ - at);
+                        std::memset(r + at, 0, k);
+                        p += k;
+                    }
                 }
                 L = Level();
             }
-            if (tt_.n) {
-                if (scratchBytes_ < maxLeft) {
-                    if (scratch_) (void)hipFree(scratch_);
-                    scratch_ = nullptr;
-                    if (hipMalloc(&scratch_, ringCap_) != hipSuccess) return ZRC4_ERR_OUT_OF_MEMORY;
-                    scratchBytes_ = ringCap_;
-                }
-                rc = zrc4_xor_ring(ctx_, ring_, ringCap_, tt_.ids.p, tt_.pos.p, scratch_, tt_.off.p, tt_.len.p,
-                                   tt_.n, sA_);
-                if (rc != ZRC4_OK) return rc;
-            }
+        } else if ((rc = zrc4_sync(ctx_, sA_)) != ZRC4_OK) {
+            return rc;
         }
         kIds_.reserve(m);
         kOff_.reserve(m);
@@ -324,40 +552,53 @@ private:
     {
         if (sB_) (void)hipStreamSynchronize(sB_);
         if (sA_) (void)hipStreamSynchronize(sA_);
-        if (evB_) (void)hipEventDestroy(evB_);
+        for (Refill &r : refill_)
+            if (r.ev) {
+                (void)hipEventDestroy(r.ev);
+                r.ev = nullptr;
+            }
         if (sA_) (void)hipStreamDestroy(sA_);
         if (sB_) (void)hipStreamDestroy(sB_);
-        if (ring_) (void)hipFree(ring_);
-        if (scratch_) (void)hipFree(scratch_);
+        for (uint8_t *&slab : ringSlab_)
+            if (slab) {
+                (void)hipHostFree(slab);
+                slab = nullptr;
+            }
         if (ctx_) zrc4_destroy(ctx_);
         sA_ = sB_ = nullptr;
-        evB_ = nullptr;
-        ring_ = scratch_ = nullptr;
         ctx_ = nullptr;
     }
 
-    static constexpr uint32_t kRefillChunk = 2048;
-    const bool debugNoRefill_ = std::getenv("ZSX_RESERVOIR_NO_REFILL") != nullptr;   // A/B knobs
+    static constexpr uint32_t kRefillChunk = 8192;
+    static constexpr uint32_t kRefillDepth = 2;
+    static constexpr int ZRC4_ERR_NOT_READY_ = 1;   // internal: oldest refill still running
+    const bool debugNoRefill_ = std::getenv("ZSX_RESERVOIR_NO_REFILL") != nullptr;   // test knobs
     const bool debugSyncRefill_ = std::getenv("ZSX_RESERVOIR_SYNC_REFILL") != nullptr;
 
     zrc4_ctx *ctx_ = nullptr;
     hipStream_t sA_ = nullptr, sB_ = nullptr;
-    hipEvent_t evB_ = nullptr;
+    Refill refill_[kRefillDepth];
+    uint32_t head_ = 0, inFlight_ = 0;
     uint8_t *base_ = nullptr;
     uint32_t ringCap_;
-    uint8_t *ring_ = nullptr;
-    uint8_t *scratch_ = nullptr;
-    uint32_t scratchBytes_ = 0;
+    uint32_t refillChunk_ = 0;
+    std::vector<uint8_t *> ringSlab_;
     std::vector<Level> level_;
-    bool refillInFlight_ = false;
-    std::vector<uint32_t> refillSlots_;
-    Table tc_, tt_, tr_, tp_[2];                // consume / drain / refill / top-up piece tables
+    std::vector<uint32_t> seen_;
+    uint32_t callStamp_ = 0;
+    std::vector<uint8_t> hungryMark_;
+    std::vector<uint32_t> hungry_;
+    std::vector<Entry> es_, rs_;
+    Table tt_;                                    // tail grouped table
+    FrameTable ft_;                               // framing tables of cryptFrame
     PinnedArray<uint32_t> kIds_, kLen_;
     PinnedArray<uint64_t> kOff_;
     PinnedArray<uint8_t> kBytes_;
     std::vector<uint32_t> seedIds_, seedLen_;
     std::vector<uint64_t> seedOff_;
     std::vector<uint8_t> keyBytes_;
+    unsigned long long ringBytes_ = 0, tailBytes_ = 0, tailLaunches_ = 0, refillBytes_ = 0, refillLaunches_ = 0,
+                       refillWaits_ = 0, framed_ = 0;
 };
 
 }  // namespace
