@@ -85,7 +85,7 @@ def shard_first(rank: int, R: int, S: int) -> int:
 class GpuRunner:
     """Owns the device buffers of R rotating batches on one GPU."""
 
-    def __init__(self, torch, device: int, S: int, L: int, R: int, first: int):
+    def __init__(self, torch, device: int, S: int, L: int, R: int, first: int, ids_mode: str = "range"):
         from zsummerx_amd import Context, synth
         self.torch, self.S, self.L, self.R = torch, S, L, R
         dev = torch.device("cuda", device)
@@ -110,17 +110,43 @@ class GpuRunner:
         self.ctx.sync(self.stream)
         # batch b = slots [b*S, (b+1)*S): zrc4_crypt_range(ctx, first_slot, payload, off, len, n, stream)
         lib, h, st = self.ctx._lib, self.ctx._h, C.c_void_p(self.stream.cuda_stream)
-        self._fn = lib.zrc4_crypt_range
         self._args = []
-        for b in range(R):
-            self._args.append((h, b * S, C.c_void_p(self.payload.data_ptr()),
-                               C.c_void_p(self.off.data_ptr() + 8 * b * S), C.c_void_p(self.len.data_ptr() + 4 * b * S),
-                               S, st))
+        if ids_mode == "range":
+            self._fn = lib.zrc4_crypt_range
+            for b in range(R):
+                self._args.append((h, b * S, C.c_void_p(self.payload.data_ptr()),
+                                   C.c_void_p(self.off.data_ptr() + 8 * b * S),
+                                   C.c_void_p(self.len.data_ptr() + 4 * b * S), S, st))
+        else:
+            # Entry i of batch b crypts session b*S + i with the slot the
+            # session was seeded in; slots are a random permutation inside each
+            # 256-slot group and the groups come in random order ("scattered"
+            # ids, as an engine's free list hands them out).  grouped: entries
+            # bucketed by group -> zrc4_crypt_grouped (coalesced images);
+            # scattered: the same ids unbucketed -> zrc4_crypt (per-lane gathers).
+            rng = np.random.default_rng(77)
+            perm = np.empty(n, dtype=np.int64)
+            for b in range(R):
+                G = -(-S // 256)
+                order = rng.permutation(G)
+                pos = 0
+                for g in order:
+                    lo, hi = b * S + g * 256, min(b * S + (g + 1) * 256, (b + 1) * S)
+                    perm[b * S + pos: b * S + pos + (hi - lo)] = lo + rng.permutation(hi - lo)
+                    pos += hi - lo
+            # entry e of batch b -> session perm[e]: keys/state/payload follow the session
+            self.ids = T(perm.astype(np.int32))
+            self.off = T((perm * L).astype(np.int64))
+            self._fn = lib.zrc4_crypt_grouped if ids_mode == "grouped" else lib.zrc4_crypt
+            for b in range(R):
+                self._args.append((h, C.c_void_p(self.ids.data_ptr() + 4 * b * S), C.c_void_p(self.payload.data_ptr()),
+                                   C.c_void_p(self.off.data_ptr() + 8 * b * S),
+                                   C.c_void_p(self.len.data_ptr() + 4 * b * S), S, st))
 
     def step(self, i: int) -> None:
         rc = self._fn(*self._args[i % self.R])
         if rc:
-            raise RuntimeError(f"zrc4_crypt_range failed: {rc}")
+            raise RuntimeError(f"zrc4 crypt ({self._fn.__name__}) failed: {rc}")
 
     def sync(self) -> None:
         self.torch.cuda.synchronize()
@@ -128,7 +154,12 @@ class GpuRunner:
     def check(self) -> None:
         self.ctx.sync(self.stream)
 
-    def timed_steps(self, first: int, k: int, every: int = 16):
+    def make_events(self, k: int, every: int = 16):
+        """The HIP events of timed_steps, created BEFORE the timed region
+        (creating one costs host time that is not part of a step)."""
+        return [self.torch.cuda.Event(enable_timing=True) for _ in range(-(-k // every) + 1)]
+
+    def timed_steps(self, first: int, k: int, every: int = 16, marks=None):
         """Launch steps first..first+k-1 back to back; HIP events on the launch
         stream bracket consecutive segments of `every` launches, and each
         segment's duration / its launch count is returned (ms per launch).
@@ -136,22 +167,26 @@ class GpuRunner:
         and reads ~3 us high on a 50 us kernel -- tools/launch_gap.py; a
         16-launch segment amortises that to <0.2 us and agrees with the
         rocprofv3 kernel average.)"""
-        torch = self.torch
-        marks, counts = [], []
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record(self.stream)
-        marks.append(ev)
-        done = 0
+        if marks is None:
+            marks = self.make_events(k, every)
+        self.launch_steps(first, k, every, marks)
+        self.sync()
+        return self.segment_ms(k, every, marks)
+
+    def launch_steps(self, first: int, k: int, every: int, marks) -> None:
+        marks[0].record(self.stream)
+        done, seg = 0, 0
         while done < k:
             m = min(every, k - done)
             for i in range(m):
                 self.step(first + done + i)
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record(self.stream)
-            marks.append(ev)
-            counts.append(m)
+            seg += 1
+            marks[seg].record(self.stream)
             done += m
-        self.sync()
+
+    @staticmethod
+    def segment_ms(k: int, every: int, marks):
+        counts = [min(every, k - d) for d in range(0, k, every)]
         return [a.elapsed_time(b) / m for a, b, m in zip(marks, marks[1:], counts)]
 
 
@@ -175,7 +210,7 @@ def run_bench(args, ws, rank, local, backend="nccl", make_runner=None):
     S = per_rank_sessions(S_job, ws) if args.strong else S_job
     R = rotation_batches(S, L, args.footprint_mib) if args.footprint_mib > 0 else 1
     if make_runner is None:
-        runner = GpuRunner(torch, local, S, L, R, shard_first(rank, R, S))
+        runner = GpuRunner(torch, local, S, L, R, shard_first(rank, R, S), getattr(args, "ids", "range"))
     else:
         runner = make_runner(S, L, R, shard_first(rank, R, S))
     dev = "cuda" if on_gpu else "cpu"
@@ -188,13 +223,15 @@ def run_bench(args, ws, rank, local, backend="nccl", make_runner=None):
         runner.step(i)
     runner.sync()
 
+    marks = runner.make_events(args.steps, args.event_every)
     barrier()
     runner.sync()
     t0 = time.perf_counter()
-    kern_ms = runner.timed_steps(args.warmup, args.steps, args.event_every)
+    runner.launch_steps(args.warmup, args.steps, args.event_every, marks)
     runner.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    kern_ms = runner.segment_ms(args.steps, args.event_every, marks)
     runner.check()
 
     t = torch.tensor([elapsed, statistics.mean(kern_ms)], dtype=torch.float64, device=dev)
@@ -267,11 +304,12 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
                    "job": ("fixed total split across ranks (strong)" if args.strong
                            else "per-GPU batch replicated over ranks' own sessions (weak)"),
                    "footprint_mib_per_gpu": round(R * S * (L + 256) / 2**20, 1),
-                   "parallelism": f"shard{ws} (sessions split across GPUs, no collective)"},
+                   "parallelism": f"shard{ws} (sessions split across GPUs, no collective)",
+                   "slot_ids": getattr(args, "ids", "range")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic,
-                     "kernel": kernel_name(S),
+                     "kernel": kernel_name(S, getattr(args, "ids", "range")),
                      "algorithmic_bytes_per_launch": B,
                      "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                      "kernel_min_segment_us": round(min(kern_ms) * 1e3, 3),
@@ -283,16 +321,21 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
     }
 
 
-def kernel_name(S: int) -> str:
-    """The kernel zrc4_crypt_range launches for S sessions (zrc4.hip
+def kernel_name(S: int, ids: str = "range") -> str:
+    """The kernel the bench's crypt call launches for S sessions (zrc4.hip
     launch_crypt): more 256-session groups than CUs -> the persistent
-    throughput kernel, otherwise one group per workgroup."""
+    throughput kernel, otherwise one group per workgroup; grouped ids always
+    take crypt_kernel<kGrouped>."""
+    if ids == "grouped":
+        return "zrc4::crypt_kernel<2, false>"
     try:
         import torch
         cus = torch.cuda.get_device_properties(0).multi_processor_count
     except Exception:
         cus = 256
     groups = -(-S // 256)
+    if ids == "scattered":
+        return "zrc4::crypt_stream_kernel<false>" if groups > cus else "zrc4::crypt_kernel<0, false>"
     return "zrc4::crypt_stream_kernel<true>" if groups > cus else "zrc4::crypt_kernel<1, false>"
 
 
@@ -623,6 +666,9 @@ def parse(argv=None):
                    help="CPU baseline time budget on rank 0 at N=1 (0 disables)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="cap on CPU-baseline threads (0 = every core in the affinity mask)")
+    p.add_argument("--ids", choices=["range", "grouped", "scattered"], default="range",
+                   help="slot addressing: contiguous range (zrc4_crypt_range), scattered slots bucketed by group "
+                        "(zrc4_crypt_grouped, the engine's path) or the same ids unbucketed (zrc4_crypt)")
     p.add_argument("--event-every", type=int, default=16,
                    help="launches per HIP-event segment (kernel duration = segment time / N)")
     p.add_argument("--host-inclusive", action="store_true",

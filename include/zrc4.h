@@ -197,6 +197,10 @@ int zrc4_crypt_grouped_frame(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payloa
 /* Wait for `stream`, then report (and clear) any latched device-side fault. */
 int zrc4_sync(zrc4_ctx *ctx, void *stream);
 
+/* Report (and clear) faults latched by kernels that have already completed
+ * (e.g. after an event query succeeded), without waiting for any stream. */
+int zrc4_poll_faults(zrc4_ctx *ctx);
+
 /* Export / import one slot's state: S-box bytes + x + y (the reference's
  * int _box[256], _x, _y narrowed to bytes; values are always in [0,255]). */
 int zrc4_get_state(zrc4_ctx *ctx, uint32_t id, uint8_t sbox[256], uint8_t *x,

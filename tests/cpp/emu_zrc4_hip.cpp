@@ -106,6 +106,7 @@ int zrc4_xor_ring(zrc4_ctx *, uint8_t *ring, uint32_t cap, const uint32_t *rid, 
     return ZRC4_OK;
 }
 int zrc4_sync(zrc4_ctx *, void *) { return ZRC4_OK; }
+int zrc4_poll_faults(zrc4_ctx *) { return ZRC4_OK; }
 const char *zrc4_strerror(int) { return "emulated zrc4"; }
 
 }  // extern "C"

@@ -55,7 +55,8 @@ def test_direct_host_logic_emulated(tools):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode,sessions,rounds,seed", [("device", 64, 300, 1), ("device", 300, 100, 7),
-                                                        ("direct", 64, 80, 2)])
+                                                        ("device", 2048, 50, 3), ("direct", 64, 80, 2),
+                                                        ("direct", 1024, 30, 4)])
 def test_device_hooks_vs_oracle(tools, mode, sessions, rounds, seed):
     run(tools / "hooks_check", mode, sessions, rounds, seed)
 

@@ -59,15 +59,23 @@ class OracleRunner:
     def check(self):
         pass
 
-    def timed_steps(self, first, k, every=1):
+    # bench.GpuRunner's timing interface: events made before the timed
+    # region, launches, then per-segment ms per step
+    def make_events(self, k, every=16):
+        return [None] * (-(-k // every) + 1)
+
+    def launch_steps(self, first, k, every, marks):
         import time
-        out = []
-        for i in range(first, first + k):
+        for seg, d in enumerate(range(0, k, every)):
             t0 = time.perf_counter()
-            self.step(i)
-            if (i - first) % every == 0:
-                out.append((time.perf_counter() - t0) * 1e3)
-        return out
+            m = min(every, k - d)
+            for i in range(first + d, first + d + m):
+                self.step(i)
+            marks[seg] = (time.perf_counter() - t0) * 1e3 / m
+
+    @staticmethod
+    def segment_ms(k, every, marks):
+        return [v for v in marks if v is not None]
 
 
 def _worker(rank, ws, port, q, workload, steps, warmup, footprint, strong=False):

@@ -51,6 +51,9 @@ def main():
     ap.add_argument("--launches", type=int, default=12)
     ap.add_argument("--footprint-mib", type=int, default=640)
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--active-waves", type=int, default=4,
+                    help="only the first k waves of every 256-session group get payload (len 0 for the rest): "
+                         "the chain rate at k waves per CU")
     args = ap.parse_args()
     from zsummerx_amd import build
     path = build.build_variant("timing", {"ZRC4_TIMING": "1"})
@@ -78,7 +81,9 @@ def main():
         koff = torch.arange(n, dtype=torch.int64, device=dev) * 16
         pay = torch.from_numpy(synth.payload(0, n * L, threads=8)).to(dev)
         off = torch.arange(n, dtype=torch.int64, device=dev) * L
-        ln = torch.full((n,), L, dtype=torch.int32, device=dev)
+        lnh = np.full(n, L, dtype=np.int32)
+        lnh.reshape(-1, 4, 64)[:, args.active_waves:, :] = 0
+        ln = torch.from_numpy(lnh).to(dev)
         h = C.c_void_p()
         _capi.check(lib.zrc4_create(C.byref(h), 0, n), "create")
         _capi.check(lib.zrc4_ksa_range(h, 0, C.c_void_p(keys.data_ptr()), C.c_void_p(koff.data_ptr()),
@@ -101,7 +106,9 @@ def main():
         if rc:
             raise SystemExit(f"hipMemcpy failed {rc}")
         waves = (S + 63) // 64
-        out[wl] = summarise(rec, waves, L)
+        act = np.array([(w % 4) < args.active_waves for w in range(waves)])
+        out[wl] = summarise(rec[:waves][act], int(act.sum()), L)
+        out[wl]["active_waves_per_group"] = args.active_waves
         print(wl, json.dumps(out[wl]), flush=True)
         lib.zrc4_destroy(h)
         del keys, adv, pay, off, ln, klen, koff, zoff

@@ -45,6 +45,7 @@ SIGNATURES = [
     ("zrc4_xor_ring", C.c_int, [_P, _P, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_frame_scan", C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P]),
     ("zrc4_sync", C.c_int, [_P, _P]),
+    ("zrc4_poll_faults", C.c_int, [_P]),
     ("zrc4_get_state", C.c_int, [_P, C.c_uint32, _U8P, _U8P, _U8P]),
     ("zrc4_set_state", C.c_int, [_P, C.c_uint32, _U8P, C.c_uint8, C.c_uint8]),
     ("zrc4_strerror", C.c_char_p, [C.c_int]),

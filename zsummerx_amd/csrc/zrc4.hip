@@ -58,7 +58,9 @@ int grow_stage(zrc4_ctx *c, size_t bytes)
     c->h_stage = nullptr;
     c->d_stage_bytes = c->h_stage_bytes = 0;
     if (hipMalloc(&c->d_stage, want) != hipSuccess) return ZRC4_ERR_OUT_OF_MEMORY;
-    if (hipHostMalloc(&c->h_stage, want, hipHostMallocDefault) != hipSuccess)
+    // coherent: small batches run on it in place, and kernels are dispatched
+    // with agent-scope acquire (a non-coherent line could be stale in L2)
+    if (hipHostMalloc(&c->h_stage, want, hipHostMallocCoherent) != hipSuccess)
         return ZRC4_ERR_OUT_OF_MEMORY;
     c->d_stage_bytes = c->h_stage_bytes = want;
     return ZRC4_OK;
@@ -137,9 +139,8 @@ int launch_ksa(zrc4_ctx *c, const uint32_t *ids, uint32_t first_slot, const uint
 // The per-iteration completion point of the session engine's hooks: ONE
 // stream wait, then the latch word is read straight from pinned memory (a
 // device-to-host copy of it used to cost another ~11 us per call).
-int check_err(zrc4_ctx *c, hipStream_t s)
+int read_faults(zrc4_ctx *c)
 {
-    ZRC4_TRY(hipStreamSynchronize(s));
     volatile uint32_t *e = c->err;
     int rc = ZRC4_OK;
     if (e[zrc4::kErrLdsLayout]) rc = ZRC4_ERR_INTERNAL;
@@ -147,6 +148,12 @@ int check_err(zrc4_ctx *c, hipStream_t s)
     else if (e[zrc4::kErrSlotRange]) rc = ZRC4_ERR_SLOT_RANGE;
     for (uint32_t i = 0; i < zrc4::kErrWords; ++i) e[i] = 0u;
     return rc;
+}
+
+int check_err(zrc4_ctx *c, hipStream_t s)
+{
+    ZRC4_TRY(hipStreamSynchronize(s));
+    return read_faults(c);
 }
 
 }  // namespace
@@ -176,7 +183,7 @@ int zrc4_create(zrc4_ctx **out, int device, uint32_t capacity)
     bool ok = hipMalloc(&c->arena, groups * (size_t)zrc4::kGroupBytes) == hipSuccess &&
               hipMalloc(&c->xy, (size_t)c->capacity * sizeof(uint16_t)) == hipSuccess &&
               hipMalloc(&c->sink, zrc4::kSinkBytes) == hipSuccess &&
-              hipHostMalloc(&c->err, zrc4::kErrWords * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc(&c->err, zrc4::kErrWords * sizeof(uint32_t), hipHostMallocCoherent) == hipSuccess &&
               hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     if (!ok) { zrc4_destroy(c); return ZRC4_ERR_OUT_OF_MEMORY; }
     // Fresh slots hold the reference's empty-key state: identity box, x = y = 0
@@ -331,6 +338,12 @@ int zrc4_frame_scan(zrc4_ctx *c, const uint8_t *buf, const uint64_t *off, const 
     hipLaunchKernelGGL(zrc4::frame_scan_kernel, dim3((n + 255u) / 256u), dim3(256), 0, (hipStream_t)stream,
                        buf, off, len, bound, n, max_packets, npk, used, status, max_packets ? pkt_len : nullptr);
     return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
+}
+
+int zrc4_poll_faults(zrc4_ctx *c)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    return read_faults(c);
 }
 
 int zrc4_sync(zrc4_ctx *c, void *stream)

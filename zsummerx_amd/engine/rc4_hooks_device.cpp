@@ -56,6 +56,27 @@
 namespace zsummerx_amd {
 namespace {
 
+// Pinned host allocations shared with the kernels (blocks, rings, batch
+// tables) are COHERENT (fine-grained).  HIP dispatches kernels with
+// agent-scope acquire/release, so a kernel can hit lines of NON-coherent host
+// memory still held in the GPU L2 from an earlier kernel after the host has
+// rewritten them (stale batch tables, SessionBlocks, zeroed ring bytes): the
+// hooks_check run at 2 048 sessions failed that way with hipHostMallocDefault
+// (profiles/r02/hooks_diag.jsonl).  Diagnostic knob:
+// ZSX_HOST_ALLOC=coherent|noncoherent|default.
+unsigned hostAllocFlags()
+{
+    static const unsigned f = [] {
+        const char *e = std::getenv("ZSX_HOST_ALLOC");
+        if (!e) return (unsigned)hipHostMallocCoherent;
+        if (!std::strcmp(e, "default")) return (unsigned)hipHostMallocDefault;
+        if (!std::strcmp(e, "coherent")) return (unsigned)hipHostMallocCoherent;
+        if (!std::strcmp(e, "noncoherent")) return (unsigned)hipHostMallocNonCoherent;
+        return (unsigned)hipHostMallocCoherent;
+    }();
+    return f;
+}
+
 template <class T>
 struct PinnedArray {
     T *p = nullptr;
@@ -66,7 +87,7 @@ struct PinnedArray {
         size_t c = cap ? cap : 1024;
         while (c < n) c *= 2;
         T *q = nullptr;
-        if (hipHostMalloc(reinterpret_cast<void **>(&q), c * sizeof(T), hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc(reinterpret_cast<void **>(&q), c * sizeof(T), hostAllocFlags()) != hipSuccess)
             throw std::bad_alloc();
         if (p) {
             std::memcpy(q, p, cap * sizeof(T));   // keep the entries already pushed
@@ -214,7 +235,7 @@ public:
     void *allocBlocks(size_t bytes) override
     {
         void *p = nullptr;
-        if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+        if (hipHostMalloc(&p, bytes, hostAllocFlags()) != hipSuccess) throw std::bad_alloc();
         if (!base_) base_ = static_cast<uint8_t *>(p);
         return p;
     }
@@ -331,7 +352,7 @@ private:
         if (!slab) {
             const size_t bytes = (size_t)ZRC4_GROUP_SLOTS * ringCap_;
             void *p = nullptr;
-            if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+            if (hipHostMalloc(&p, bytes, hostAllocFlags()) != hipSuccess) throw std::bad_alloc();
             std::memset(p, 0, bytes);
             slab = static_cast<uint8_t *>(p);
         }
@@ -410,7 +431,7 @@ private:
             if ((rc = drainRefills()) != ZRC4_OK) return rc;     // slot state must be quiet
             if ((rc = runTail(es_)) != ZRC4_OK) return rc;
         }
-        while (inFlight_ < kRefillDepth) {
+        while (inFlight_ < refillDepth_) {
             const uint32_t before = inFlight_;
             if ((rc = launchRefill()) != ZRC4_OK) return rc;
             if (inFlight_ == before) break;
@@ -427,7 +448,7 @@ private:
     // slot's pieces sequential).
     int launchRefill()
     {
-        if (inFlight_ >= kRefillDepth || debugNoRefill_ || hungry_.empty()) return ZRC4_OK;
+        if (inFlight_ >= refillDepth_ || debugNoRefill_ || hungry_.empty()) return ZRC4_OK;
         Refill &R = refill_[(head_ + inFlight_) % kRefillDepth];
         rs_.clear();
         R.ends.clear();
@@ -499,7 +520,9 @@ private:
             if (rc != ZRC4_OK) return rc;
             any = true;
         }
-        return any ? zrc4_sync(ctx_, sB_) : ZRC4_OK;
+        // committed refills have completed: their faults are in the latch
+        // (no stream wait -- a second queued refill keeps running)
+        return any ? zrc4_poll_faults(ctx_) : ZRC4_OK;
     }
     int drainRefills() { return pollRefills(true); }
 
@@ -571,6 +594,7 @@ private:
 
     static constexpr uint32_t kRefillChunk = 8192;
     static constexpr uint32_t kRefillDepth = 2;
+    const uint32_t refillDepth_ = std::getenv("ZSX_REFILL_DEPTH") ? std::max(1, std::min(2, std::atoi(std::getenv("ZSX_REFILL_DEPTH")))) : kRefillDepth;
     static constexpr int ZRC4_ERR_NOT_READY_ = 1;   // internal: oldest refill still running
     const bool debugNoRefill_ = std::getenv("ZSX_RESERVOIR_NO_REFILL") != nullptr;   // test knobs
     const bool debugSyncRefill_ = std::getenv("ZSX_RESERVOIR_SYNC_REFILL") != nullptr;
