@@ -282,7 +282,8 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
     value = total_payload / tmax / GIB
     B = algorithmic_bytes(S, L)
     achieved = B / (kern_avg_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.workload)
+    ids = getattr(args, "ids", "range")
+    traffic = load_traffic(args.workload if ids == "range" else f"{args.workload}-{ids}")
     return {
         "metric": METRIC,
         "value": round(value, 3),
@@ -334,6 +335,8 @@ def kernel_name(S: int, ids: str = "range") -> str:
     except Exception:
         cus = 256
     groups = -(-S // 256)
+    if ids == "range" and 2 * groups <= cus:
+        return "zrc4::crypt_half_kernel<false>"
     if ids == "scattered":
         return "zrc4::crypt_stream_kernel<false>" if groups > cus else "zrc4::crypt_kernel<0, false>"
     return "zrc4::crypt_stream_kernel<true>" if groups > cus else "zrc4::crypt_kernel<1, false>"

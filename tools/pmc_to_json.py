@@ -30,7 +30,7 @@ def per_dispatch(path, name_filter):
     return [(names[d], agg[d]) for d in sorted(agg)]
 
 
-def main(src="gpurun_out/traffic", tag="r01"):
+def main(src="gpurun_out/traffic", tag="r02"):
     src = ROOT / src
     calib = per_dispatch(src / "calib_FETCH_SIZE" / "run_counter_collection.csv", "calib_load_lane")
     calib_bytes = 1 << 30
@@ -40,7 +40,7 @@ def main(src="gpurun_out/traffic", tag="r01"):
         wr = per_dispatch(src / f"{wl}_WRITE_SIZE" / "run_counter_collection.csv", "zrc4::crypt_")[1:]
         f, w = [v for _, v in fr], [v for _, v in wr]
         kname = collections.Counter(n.split("(")[0].replace("void ", "") for n, _ in fr).most_common(1)[0][0]
-        S, L = SHAPES[wl]
+        S, L = SHAPES[wl.split("-")[0]]
         fb, wb = statistics.median(f) * 1024, statistics.median(w) * 1024
         out = {
             "kernel": kname, "workload": wl, "dispatches": len(f),
@@ -50,7 +50,8 @@ def main(src="gpurun_out/traffic", tag="r01"):
             "hbm_bytes_per_launch": round(fb / fetch_factor + wb),
             "algorithmic_bytes_per_launch": 2 * S * L + 516 * S,
             "source": f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) over "
-                      f"bench.py --workload {wl} --steps 20; calibrated with tools/ubench/traffic_calib.hip",
+                      f"bench.py --workload {wl.split('-')[0]} --ids {(wl.split('-') + ['range'])[1]} --steps 20; "
+                      f"calibrated with tools/ubench/traffic_calib.hip",
             "round": tag,
         }
         out["traffic_over_algorithmic"] = round(out["hbm_bytes_per_launch"] / out["algorithmic_bytes_per_launch"], 3)

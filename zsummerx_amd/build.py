@@ -170,6 +170,15 @@ def build_test_tools(force: bool = False, sanitize: bool = False) -> Path:
     return out
 
 
+def build_ubench(force: bool = False) -> None:
+    """tools/ubench/traffic_calib: the known-byte-count kernels the PMC
+    traffic passes calibrate FETCH_SIZE against (scripts/pmc_traffic.sh)."""
+    src = ROOT / "tools" / "ubench" / "traffic_calib.hip"
+    out = src.with_suffix("")
+    if force or _stale(out, [src]):
+        subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-O2", "-o", str(out), str(src)], check=True)
+
+
 def build_oracle() -> None:
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
 
@@ -180,6 +189,7 @@ def build_all(force: bool = False) -> None:
     build_frame(force)
     build_oracle()
     build_test_tools(force)
+    build_ubench(force)
 
 
 if __name__ == "__main__":

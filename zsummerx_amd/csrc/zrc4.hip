@@ -12,6 +12,10 @@
 #include <algorithm>
 #include <new>
 
+#ifndef ZRC4_HALF
+#define ZRC4_HALF 1   // A/B knob: 0 runs few-group range batches on whole-group workgroups too
+#endif
+
 struct zrc4_ctx {
     int device;
     int num_cus;
@@ -86,6 +90,19 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
     const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
     const dim3 blk(zrc4::kGroup);
     const bool stream_kernel = mode != zrc4::kGrouped && grid > (uint32_t)c->num_cus;
+    // Few whole groups: half-group workgroups, one per CU (2 waves per CU).
+    const bool half = ZRC4_HALF && mode == zrc4::kRange && (first_slot & 255u) == 0u &&
+                      2u * grid <= (uint32_t)c->num_cus;
+    const dim3 hblk(zrc4::kGroup / 2), hgrid((n + zrc4::kGroup / 2 - 1) / (zrc4::kGroup / 2));
+    if (half) {
+        if (fr)
+            hipLaunchKernelGGL(zrc4::crypt_half_kernel<true>, hgrid, hblk, 0, s, c->arena, c->xy, first_slot,
+                               payload, off, len, n, c->capacity, c->err, c->sink, *fr);
+        else
+            hipLaunchKernelGGL(zrc4::crypt_half_kernel<false>, hgrid, hblk, 0, s, c->arena, c->xy, first_slot,
+                               payload, off, len, n, c->capacity, c->err, c->sink, zrc4::FrameArgs{});
+        return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
+    }
     if (fr && !stream_kernel) {
         if (mode == zrc4::kRange)
             hipLaunchKernelGGL((zrc4::crypt_kernel<zrc4::kRange, true>), dim3(grid), blk, 0, s, c->arena, c->xy,

@@ -73,7 +73,7 @@ __device__ __forceinline__ uint32_t col_of(uint32_t j)
 // Diagnostic timing build (ZRC4_TIMING=1, never the product): lane 0 of each
 // wave stamps s_memrealtime (100 MHz) and s_memtime (shader clock) at kernel
 // entry, S-boxes in LDS, keystream done, and state stored; the 64-byte record
-// of wave w of workgroup b goes to sink + ((b * 4 + w) & 1023) * 64
+// of global wave w (thread index / 64) goes to sink + (w & 1023) * 64
 // (zrc4_debug_sink exports the sink in such builds; tools/kernel_timeline.py).
 // ---------------------------------------------------------------------------
 #ifndef ZRC4_TIMING
@@ -93,7 +93,7 @@ __device__ __forceinline__ void stamps_out(const Stamps &s, uint8_t *sink)
 {
 #if ZRC4_TIMING
     if ((threadIdx.x & 63u) == 0u) {
-        uint64_t *o = reinterpret_cast<uint64_t *>(sink + (((blockIdx.x * 4u + (threadIdx.x >> 6)) & 1023u) * 64u));
+        uint64_t *o = reinterpret_cast<uint64_t *>(sink + ((((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & 1023u) * 64u));
         for (int i = 0; i < 4; ++i) {
             o[i] = s.r[i];
             o[4 + i] = s.c[i];
@@ -596,11 +596,19 @@ __device__ __forceinline__ void crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8
 
 // One group's 64 KiB S-box image, 16 x 16 B per lane into v160..v223, issued
 // from asm and NOT waited for (the caller waits with a counted vmcnt).
-__device__ __forceinline__ void issue_image_asm(u32x32 &ilo, u32x32 &ihi, const uint8_t *ibase)
+// vo0 = the lane's byte offset in the first 4 KiB of the image; load i reads
+// vo0 + i * 4 KiB (whole group: 16 * tid; half group h: rows of 16 lanes x
+// 16 B starting at byte 128 * h of every 256-B row, image_lane_offset).
+__device__ __forceinline__ uint32_t image_lane_offset(uint32_t tid, bool half, uint32_t h)
+{
+    return half ? ((tid >> 3) << 8) | (h << 7) | ((tid & 7u) << 4) : tid << 4;
+}
+
+__device__ __forceinline__ void issue_image_asm(u32x32 &ilo, u32x32 &ihi, const uint8_t *ibase, uint32_t vo0)
 {
     uint32_t vo;
     asm volatile(
-        "v_lshlrev_b32 %[vo], 4, %[j]\n\t"
+        "v_mov_b32 %[vo], %[j]\n\t"
         "global_load_dwordx4 v[160:163], %[vo], %[ib]\n\t"
         "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
         "global_load_dwordx4 v[164:167], %[vo], %[ib]\n\t"
@@ -633,15 +641,14 @@ __device__ __forceinline__ void issue_image_asm(u32x32 &ilo, u32x32 &ihi, const 
         "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
         "global_load_dwordx4 v[220:223], %[vo], %[ib]\n\t"
         : "=&{v[160:191]}"(ilo), "=&{v[192:223]}"(ihi), [vo] "=&v"(vo)
-        : [ib] "s"(ibase), [j] "v"(threadIdx.x)
+        : [ib] "s"(ibase), [j] "v"(vo0)
         : "memory");
 }
 
 // ---------------------------------------------------------------------------
-// crypt_kernel: batched RC4Encryption::encryption, one group per workgroup
-// (launches with at most one group per CU: the chain-bound regime).
-// grid = ceil(n / 256) workgroups of 256 threads; workgroup w handles batch
-// entries [w*256, w*256+256).  How entry e maps to a slot (MODE):
+// crypt_kernel: batched RC4Encryption::encryption, one group (or, HALF, one
+// half group) per workgroup: launches with at most one group per CU, the
+// chain-bound regime.  How batch entry e maps to a slot (MODE):
 //   kRange    slot = first_slot + e (ids == NULL; the bench's and the
 //             engine's contiguous batches).  The slot is arithmetic and the
 //             host has checked first_slot + n <= capacity, so the group image
@@ -649,16 +656,25 @@ __device__ __forceinline__ void issue_image_asm(u32x32 &ilo, u32x32 &ihi, const 
 //             another: one HBM round trip); the first payload block is
 //             issued after a counted wait, so its round trip overlaps the LDS
 //             fill.  Whole (coalesced image) iff first_slot % 256 == 0.
-//   kGrouped  slot = ids[e]; the caller promises bucket w's non-idle entries
-//             all lie in ONE 256-slot group that no other bucket of the call
-//             touches (zrc4_crypt_grouped).  The group image moves as one
-//             coalesced copy and lane j runs in column col_of(slot & 255),
-//             so any subset of a group in any order costs what a whole group
-//             costs.  A bucket that mixes groups latches kErrGroup and is
+//   kGrouped  slot = ids[e]; the caller promises bucket w's busy entries all
+//             lie in ONE 256-slot group that no other bucket of the call
+//             touches (zrc4_crypt_grouped).  The entries are permuted through
+//             LDS so that lane j runs slot g*256 + j (its own, bank-conflict
+//             free column; running entries in their given order put lanes of
+//             one half-wave on the same LDS banks: cfg2 73.6 vs 48.9 us), and
+//             the group image moves as one coalesced copy, so any subset of a
+//             group in any order costs what a whole group costs.  A bucket
+//             that mixes groups (or repeats a slot) latches kErrGroup and is
 //             skipped.
 //   kIds      slot = ids[e], arbitrary: whole iff the 256 ids are exactly
 //             g*256 .. g*256+255 in order, otherwise each lane gathers and
 //             scatters its own 256-byte column (correct, strided).
+// HALF (kRange, first_slot % 256 == 0, few groups): 128-thread workgroups,
+// each owning the two waves of a group whose S-boxes share the dwords of one
+// 128-byte half of every image row (col_of: (wave >> 1) picks the half), so
+// each moves a 32 KiB half image.  The workgroup reserves more LDS than it
+// uses so that no two share a CU: at 2 waves per CU a chain step takes
+// 41.2 us per KiB against 43.1 at 4 (profiles/r02/tl_waves.log).
 // ---------------------------------------------------------------------------
 enum CryptMode : int { kIds = 0, kRange = 1, kGrouped = 2 };
 
@@ -708,105 +724,159 @@ __device__ __forceinline__ void frame_walk(const uint8_t *b, uint32_t L, uint32_
     status[e] = st;
 }
 
-template <int MODE, bool FRAME = false>
-__global__ void __launch_bounds__(256, 2)
-crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
-             const uint32_t *__restrict__ ids, uint32_t first_slot,
-             uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
-             const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
-             uint32_t *__restrict__ err, uint8_t *__restrict__ sink, FrameArgs fr = FrameArgs{})
+// LDS of crypt_kernel: the 64 KiB S-box image at offset 0 (the asm's absolute
+// addresses), then 16 B of flags, then the kGrouped entry table (slot -> entry
+// index / length / offset).  HALF pads the allocation past 80 KiB so that a
+// CU holds one workgroup.
+constexpr uint32_t kTabOff = kGroupBytes + 16;
+constexpr uint32_t kSmemDirect = kTabOff + 256 * 16;          // 69 648 B: two workgroups per CU
+constexpr uint32_t kSmemHalf = 96 * 1024;                     // one workgroup per CU
+
+template <int MODE, bool FRAME, bool HALF>
+__device__ __forceinline__ void
+crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
+           const uint32_t *__restrict__ ids, uint32_t first_slot,
+           uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
+           const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
+           uint32_t *__restrict__ err, uint8_t *__restrict__ sink, const FrameArgs &fr)
 {
-    // one LDS object: the 64 KiB S-box image, then 16 B of workgroup flags
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kGroupBytes + 16];
+    static_assert(!HALF || MODE == kRange, "half-group workgroups are range batches");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[HALF ? kSmemHalf : kSmemDirect];
     uint8_t *S = smem;
     if (!lds_base_ok(S, err)) return;
     Stamps ts;
     stamp(ts, 0);
 
-    const uint32_t j = threadIdx.x;
-    const uint32_t e = blockIdx.x * kGroup + j;
+    constexpr uint32_t kLanes = HALF ? 128u : 256u;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t e = blockIdx.x * kLanes + tid;        // batch entry of this thread
     const bool valid = e < n;
+    const uint32_t h = HALF ? (blockIdx.x & 1u) : 0u;    // half of the group (HALF)
+    const uint32_t j = h * 128u + tid;                   // group lane
+    const uint32_t vo0 = image_lane_offset(tid, HALF, h);
+    const uint32_t col = col_of(j);
+    volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(smem + kGroupBytes);
     uint4 img[16];
     u32x32 ilo, ihi;
+
+    bool whole;
+    uint32_t g, slot, mylen, ent;   // ent: the batch entry this lane runs (kGrouped permutes)
+    uint64_t myoff;
+    uint16_t sxy;
     if constexpr (MODE == kRange) {
         // Issued from asm, first: hipcc otherwise sinks these loads below its
         // wait for len/off.  Group (first_slot >> 8) + w lies inside the arena
         // even when first_slot is unaligned and the image goes unused.
-        issue_image_asm(ilo, ihi, arena + (size_t)((first_slot >> 8) + blockIdx.x) * kGroupBytes);
-    }
-    const uint32_t mylen0 = valid ? len[e] : 0u;
-    const uint64_t myoff = valid ? off[e] : 0u;
-    uint32_t slot;
-    if constexpr (MODE == kRange) {
-        slot = valid ? first_slot + e : ZRC4_INVALID;
-    } else {
-        slot = valid ? ids[e] : ZRC4_INVALID;
-        // kGrouped pads buckets with ZRC4_IDLE_SLOT (0xFFFFFFFF) entries
-        if (valid && slot >= capacity && !(MODE == kGrouped && slot == ZRC4_INVALID)) {
-            latch_fault(err, kErrSlotRange);
-            slot = ZRC4_INVALID;
-        }
-    }
-    const bool active = slot != ZRC4_INVALID;
-    const uint32_t mylen = active ? mylen0 : 0u;
-    const uint16_t sxy = (MODE == kRange ? active : (active && mylen)) ? xy[slot] : (uint16_t)0;
-
-    bool whole;
-    uint32_t g;
-    uint32_t col = col_of(j);
-    volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(smem + kGroupBytes);
-    if constexpr (MODE == kRange) {
+        g = (first_slot >> 8) + (HALF ? blockIdx.x >> 1 : blockIdx.x);
+        issue_image_asm(ilo, ihi, arena + (size_t)g * kGroupBytes, vo0);
         whole = (first_slot & 255u) == 0u;
-        g = (first_slot >> 8) + blockIdx.x;
+        ent = e;
+        mylen = valid ? len[e] : 0u;
+        myoff = valid ? off[e] : 0u;
+        slot = valid ? first_slot + e : ZRC4_INVALID;
+        sxy = valid ? xy[slot] : (uint16_t)0;
     } else if constexpr (MODE == kGrouped) {
-        // the bucket's group: min and max group of its busy entries must agree
-        if (j == 0) {
+        // 1. this thread's entry; 2. the bucket's group (min and max group of
+        //    its busy entries must agree) and the slot -> entry table; 3. lane
+        //    j takes the entry of slot g*256 + j.
+        uint32_t *te = reinterpret_cast<uint32_t *>(smem + kTabOff);          // entry index
+        uint32_t *tl = te + 256;                                              // length
+        uint64_t *to = reinterpret_cast<uint64_t *>(smem + kTabOff + 2048);   // offset
+        uint32_t id = valid ? ids[e] : ZRC4_INVALID;
+        const uint32_t elen = valid ? len[e] : 0u;
+        const uint64_t eoff = valid ? off[e] : 0u;
+        if (valid && id >= capacity && id != ZRC4_INVALID) {    // ZRC4_IDLE_SLOT pads buckets
+            latch_fault(err, kErrSlotRange);
+            id = ZRC4_INVALID;
+        }
+        const bool busy = id != ZRC4_INVALID && elen != 0u;
+        // Speculative image (and x/y) issue: every busy entry of a wave must
+        // lie in the bucket's group, so the wave's first busy id names it and
+        // the image load overlaps the table build below.  A wave with no busy
+        // entry (or a wrong guess: a contract violation, refused below) loads
+        // again once the group is known.
+        const uint64_t bm = __ballot(busy);
+        const uint32_t gw = bm ? (__builtin_amdgcn_readlane(id, (int)__builtin_ctzll(bm)) >> 8) : 0u;
+        issue_image_asm(ilo, ihi, arena + (size_t)gw * kGroupBytes, vo0);
+        const uint16_t xyw = xy[gw * 256u + j];
+        te[tid] = ZRC4_INVALID;
+        if (tid == 0) {
             flag[0] = 0xFFFFFFFFu;
             flag[1] = 0u;
+            flag[2] = 0u;
         }
         __syncthreads();
-        const bool busy = active && mylen;
         if (busy) {
-            atomicMin(const_cast<uint32_t *>(flag), slot >> 8);
-            atomicMax(const_cast<uint32_t *>(flag + 1), slot >> 8);
+            atomicMin(const_cast<uint32_t *>(flag), id >> 8);
+            atomicMax(const_cast<uint32_t *>(flag + 1), id >> 8);
+            if (atomicExch(&te[id & 255u], e) != ZRC4_INVALID) flag[2] = 1u;   // a slot twice
+            tl[id & 255u] = elen;
+            to[id & 255u] = eoff;
         }
         __syncthreads();
-        const uint32_t gmin = flag[0], gmax = flag[1];
-        __syncthreads();
-        if (gmin == 0xFFFFFFFFu) {                        // an idle bucket: nothing to decrypt
-            if constexpr (FRAME) {
-                if (valid) frame_walk(payload + fr.off[e], fr.len[e], fr.bound, fr.maxp, e, fr.npk, fr.used,
-                                      fr.status, fr.pkt_len);
+        const uint32_t gmin = flag[0], gmax = flag[1], dup = flag[2];
+        if (gmin == 0xFFFFFFFFu || gmin != gmax || dup) {
+            if (gmin != 0xFFFFFFFFu && tid == 0) latch_fault(err, kErrGroup);
+            if constexpr (FRAME) {                       // an idle bucket still reports its framing
+                if (valid && gmin == 0xFFFFFFFFu)
+                    frame_walk(payload + fr.off[e], fr.len[e], fr.bound, fr.maxp, e, fr.npk, fr.used, fr.status,
+                               fr.pkt_len);
             }
             return;
         }
-        if (gmin != gmax) {
-            if (j == 0) latch_fault(err, kErrGroup);
-            return;
-        }
+        g = __builtin_amdgcn_readfirstlane(gmin);       // uniform (an SGPR base for the asm loads)
         whole = true;
-        g = gmin;
-        col = col_of(slot & 255u);
+        ent = te[j];
+        mylen = ent != ZRC4_INVALID ? tl[j] : 0u;
+        myoff = ent != ZRC4_INVALID ? to[j] : 0u;
+        slot = g * 256u + j;
+        sxy = xyw;
+        if (!bm || gw != g) {                            // wave-uniform: the guess missed
+            asm volatile("s_waitcnt vmcnt(0)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
+            issue_image_asm(ilo, ihi, arena + (size_t)g * kGroupBytes, vo0);
+            sxy = xy[slot];
+        }
+        if (!mylen) sxy = 0;
+        if constexpr (FRAME) {
+            // entries that decrypt nothing are framed by their own thread now
+            if (valid && !busy)
+                frame_walk(payload + fr.off[e], fr.len[e], fr.bound, fr.maxp, e, fr.npk, fr.used, fr.status,
+                           fr.pkt_len);
+        }
     } else {
+        ent = e;
+        slot = valid ? ids[e] : ZRC4_INVALID;
+        if (valid && slot >= capacity) {
+            latch_fault(err, kErrSlotRange);
+            slot = ZRC4_INVALID;
+        }
+        mylen = slot != ZRC4_INVALID ? len[e] : 0u;
+        myoff = slot != ZRC4_INVALID ? off[e] : 0u;
+        sxy = mylen ? xy[slot] : (uint16_t)0;
         const uint32_t first = ids[blockIdx.x * kGroup];
         g = first >> 8;
-        if (j == 0) flag[0] = 1u;
+        if (tid == 0) flag[0] = 1u;
         __syncthreads();
-        if (!(active && slot == ((first & ~255u) + j) && (first & 255u) == 0u)) flag[0] = 0u;
+        if (!(slot != ZRC4_INVALID && slot == ((first & ~255u) + j) && (first & 255u) == 0u)) flag[0] = 0u;
         __syncthreads();
         whole = flag[0] != 0u;
         __syncthreads();
     }
+    const bool active = slot != ZRC4_INVALID && mylen != 0u;
 
     uint8_t *msg = payload + myoff;
     uint4 A[4];
     const bool pre = active && mylen >= 64u && head_bytes(msg, mylen) == 0u;
-    if constexpr (MODE == kRange) {
-        // The image was issued before len, off and x/y (3 loads).  Waited on
-        // every path (the registers must not be reused while it is in
-        // flight); the first payload block is issued after this wait, so its
-        // round trip overlaps the LDS fill.
-        asm volatile("s_waitcnt vmcnt(3)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
+    if constexpr (MODE != kIds) {
+        // The image was issued before the entry loads still in flight (kRange:
+        // len, off and x/y; kGrouped: x/y).  Waited on every path (the
+        // registers must not be reused while it is in flight); the first
+        // payload block is issued after this wait, so its round trip overlaps
+        // the LDS fill.
+        if constexpr (MODE == kRange)
+            asm volatile("s_waitcnt vmcnt(3)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
+        else   // the x/y load is conditional: wait for everything
+            asm volatile("s_waitcnt vmcnt(0)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             img[i] = make_uint4(ilo[4 * i], ilo[4 * i + 1], ilo[4 * i + 2], ilo[4 * i + 3]);
@@ -814,23 +884,22 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         }
     }
     if (whole) {
-        if constexpr (MODE != kRange) {
+        if constexpr (MODE == kIds) {
             const uint4 *src = reinterpret_cast<const uint4 *>(arena + (size_t)g * kGroupBytes);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) img[i] = src[i * 256 + j];
+            for (int i = 0; i < 16; ++i) img[i] = src[i * 256 + tid];
         }
         if (pre) issue_block_asm(A, msg);
-        uint4 *dst = reinterpret_cast<uint4 *>(S);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) dst[i * 256 + j] = img[i];
+        for (int i = 0; i < 16; ++i) *reinterpret_cast<uint4 *>(S + i * 4096 + vo0) = img[i];
         __syncthreads();
     } else {
         if (pre) issue_block_asm(A, msg);
-        if (active && mylen) gather_column(S, col, arena, slot);
+        if (active) gather_column(S, col, arena, slot);
     }
     stamp(ts, 1);
 
-    if (active && mylen) {
+    if (active) {
         Rc4Lane st;
         lane_init(st, S, col, sxy);
         crypt_message(S, st, msg, mylen, A, pre);
@@ -839,9 +908,10 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     if constexpr (FRAME) {
         // The lane's own decrypted bytes: its stores must have landed before
         // it reads the headers back.
-        if (valid) {
+        const bool mine = MODE == kGrouped ? (ent != ZRC4_INVALID && mylen != 0u) : valid;
+        if (mine) {
             __builtin_amdgcn_s_waitcnt(0);
-            frame_walk(payload + fr.off[e], fr.len[e], fr.bound, fr.maxp, e, fr.npk, fr.used, fr.status,
+            frame_walk(payload + fr.off[ent], fr.len[ent], fr.bound, fr.maxp, ent, fr.npk, fr.used, fr.status,
                        fr.pkt_len);
         }
     }
@@ -849,8 +919,11 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 
     if (whole) {
         __syncthreads();
-        lds_to_image(arena + (size_t)g * kGroupBytes, S);
-    } else if (active && mylen) {
+        uint8_t *img_out = arena + (size_t)g * kGroupBytes;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            *reinterpret_cast<uint4 *>(img_out + i * 4096 + vo0) = *reinterpret_cast<const uint4 *>(S + i * 4096 + vo0);
+    } else if (active) {
         scatter_column(arena, slot, S, col);
     }
 #if ZRC4_TIMING
@@ -858,6 +931,28 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     stamp(ts, 3);
     stamps_out(ts, sink);
 #endif
+}
+
+template <int MODE, bool FRAME = false>
+__global__ void __launch_bounds__(256, 2)
+crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
+             const uint32_t *__restrict__ ids, uint32_t first_slot,
+             uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
+             const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
+             uint32_t *__restrict__ err, uint8_t *__restrict__ sink, FrameArgs fr = FrameArgs{})
+{
+    crypt_body<MODE, FRAME, false>(arena, xy, ids, first_slot, payload, off, len, n, capacity, err, sink, fr);
+}
+
+// Half-group workgroups (kRange, few groups): 128 threads, one per CU.
+template <bool FRAME = false>
+__global__ void __launch_bounds__(128, 1)
+crypt_half_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uint32_t first_slot,
+                  uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
+                  const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
+                  uint32_t *__restrict__ err, uint8_t *__restrict__ sink, FrameArgs fr = FrameArgs{})
+{
+    crypt_body<kRange, FRAME, true>(arena, xy, nullptr, first_slot, payload, off, len, n, capacity, err, sink, fr);
 }
 
 // ---------------------------------------------------------------------------
