@@ -367,16 +367,20 @@ def grouped_batch(rng, n_groups, groups_total, fill=(1, 256)):
     return ids
 
 
-@pytest.mark.parametrize("fill", [(256, 256), (1, 256)])
-def test_grouped_ids_bit_exact(built, torch_cuda, fill):
+@pytest.mark.parametrize("fill,nb,trunc", [((256, 256), 64, 0), ((1, 256), 64, 0), ((1, 256), 200, 0),
+                                           ((1, 200), 64, 100), ((1, 256), 200, 37)])
+def test_grouped_ids_bit_exact(built, torch_cuda, fill, nb, trunc):
     """zrc4_crypt_grouped: each bucket a subset of ONE group, in any order,
     groups in random order, idle padding; two calls in a row continue the
-    keystream.  Checked against the oracle, every session that ran and every
-    state; slots outside the batch keep their state."""
+    keystream.  nb = 64 buckets runs half-group workgroups, 200 whole-group
+    ones; trunc drops the last entries of the batch (a short last bucket whose
+    slots still fall in both halves of its group).  Checked against the
+    oracle, every session that ran and every state; slots outside the batch
+    keep their state."""
     torch = torch_cuda
     from zsummerx_amd._capi import IDLE_SLOT
-    rng = np.random.default_rng(41 + fill[0])
-    G, nb = 96, 64                                 # 96 groups in the arena, 64 buckets per call
+    rng = np.random.default_rng(41 + fill[0] + nb + trunc)
+    G = 256                                        # groups in the arena
     cap = 256 * G
     keys = rng.integers(0, 256, 16 * cap, dtype=np.uint8)
     koff = np.arange(cap, dtype=np.uint64) * 16
@@ -390,8 +394,19 @@ def test_grouped_ids_bit_exact(built, torch_cuda, fill):
         touched = set()
         for call in range(2):
             ids = grouped_batch(rng, nb, G, fill)
+            if trunc:   # the short bucket keeps an upper-half slot of its group (entry 0)
+                last = ids[256 * (nb - 1):]
+                used = [int(v) for v in last[last != IDLE_SLOT]]
+                g = used[0] // 256
+                up = [v for v in used if v % 256 >= 128]
+                slot = up[0] if up else next(g * 256 + k for k in range(128, 256) if g * 256 + k not in used)
+                last[last == slot] = IDLE_SLOT
+                last[0] = slot
+                ids = ids[:ids.size - trunc].copy()
             busy = ids != IDLE_SLOT
             L = np.where(busy, rng.integers(0, 600, ids.size), 0).astype(np.uint32)
+            if trunc:
+                L[256 * (nb - 1)] = 333
             off = (np.arange(ids.size, dtype=np.uint64) * 640 + rng.integers(0, 16, ids.size).astype(np.uint64))
             data = rng.integers(0, 256, ids.size * 640 + 64, dtype=np.uint8)
             # oracle: per slot, in batch order (each slot once per call)

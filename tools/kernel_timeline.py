@@ -51,6 +51,9 @@ def main():
     ap.add_argument("--launches", type=int, default=12)
     ap.add_argument("--footprint-mib", type=int, default=640)
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--ids", choices=("range", "grouped"), default="range",
+                    help="grouped: slots permuted inside each group, groups in random order (bench.py --ids grouped) "
+                         "through zrc4_crypt_grouped")
     ap.add_argument("--active-waves", type=int, default=4,
                     help="only the first k waves of every 256-session group get payload (len 0 for the rest): "
                          "the chain rate at k waves per CU")
@@ -80,7 +83,18 @@ def main():
         klen = torch.full((n,), 16, dtype=torch.int32, device=dev)
         koff = torch.arange(n, dtype=torch.int64, device=dev) * 16
         pay = torch.from_numpy(synth.payload(0, n * L, threads=8)).to(dev)
-        off = torch.arange(n, dtype=torch.int64, device=dev) * L
+        perm = np.arange(n, dtype=np.int64)
+        if args.ids == "grouped":
+            rng = np.random.default_rng(77)
+            for b in range(R):
+                G = -(-S // 256)
+                pos = 0
+                for g in rng.permutation(G):
+                    lo, hi = b * S + g * 256, min(b * S + (g + 1) * 256, (b + 1) * S)
+                    perm[b * S + pos: b * S + pos + (hi - lo)] = lo + rng.permutation(hi - lo)
+                    pos += hi - lo
+        ids = torch.from_numpy(perm.astype(np.int32)).to(dev)
+        off = torch.from_numpy(perm * L).to(dev)
         lnh = np.full(n, L, dtype=np.int32)
         lnh.reshape(-1, 4, 64)[:, args.active_waves:, :] = 0
         ln = torch.from_numpy(lnh).to(dev)
@@ -95,9 +109,14 @@ def main():
         torch.cuda.synchronize()
         for i in range(args.launches):
             b = i % R
-            _capi.check(lib.zrc4_crypt_range(h, b * S, C.c_void_p(pay.data_ptr()),
-                                             C.c_void_p(off.data_ptr() + 8 * b * S),
-                                             C.c_void_p(ln.data_ptr() + 4 * b * S), S, st))
+            if args.ids == "grouped":
+                _capi.check(lib.zrc4_crypt_grouped(h, C.c_void_p(ids.data_ptr() + 4 * b * S),
+                                                   C.c_void_p(pay.data_ptr()), C.c_void_p(off.data_ptr() + 8 * b * S),
+                                                   C.c_void_p(ln.data_ptr() + 4 * b * S), S, st))
+            else:
+                _capi.check(lib.zrc4_crypt_range(h, b * S, C.c_void_p(pay.data_ptr()),
+                                                 C.c_void_p(off.data_ptr() + 8 * b * S),
+                                                 C.c_void_p(ln.data_ptr() + 4 * b * S), S, st))
         _capi.check(lib.zrc4_sync(h, st))
         sink = C.c_void_p()
         _capi.check(lib.zrc4_debug_sink(h, C.byref(sink)))
@@ -109,9 +128,10 @@ def main():
         act = np.array([(w % 4) < args.active_waves for w in range(waves)])
         out[wl] = summarise(rec[:waves][act], int(act.sum()), L)
         out[wl]["active_waves_per_group"] = args.active_waves
+        out[wl]["ids"] = args.ids
         print(wl, json.dumps(out[wl]), flush=True)
         lib.zrc4_destroy(h)
-        del keys, adv, pay, off, ln, klen, koff, zoff
+        del keys, adv, pay, off, ids, ln, klen, koff, zoff
         torch.cuda.empty_cache()
     print(json.dumps(out))
 

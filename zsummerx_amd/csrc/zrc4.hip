@@ -91,16 +91,29 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
     const dim3 blk(zrc4::kGroup);
     const bool stream_kernel = mode != zrc4::kGrouped && grid > (uint32_t)c->num_cus;
     // Few whole groups: half-group workgroups, one per CU (2 waves per CU).
-    const bool half = ZRC4_HALF && mode == zrc4::kRange && (first_slot & 255u) == 0u &&
-                      2u * grid <= (uint32_t)c->num_cus;
-    const dim3 hblk(zrc4::kGroup / 2), hgrid((n + zrc4::kGroup / 2 - 1) / (zrc4::kGroup / 2));
+    // A grouped bucket's slots may sit in either half whatever its entry
+    // count, so it always gets both halves.
+    const bool half = ZRC4_HALF && 2u * grid <= (uint32_t)c->num_cus &&
+                      ((mode == zrc4::kRange && (first_slot & 255u) == 0u) || mode == zrc4::kGrouped);
     if (half) {
-        if (fr)
-            hipLaunchKernelGGL(zrc4::crypt_half_kernel<true>, hgrid, hblk, 0, s, c->arena, c->xy, first_slot,
-                               payload, off, len, n, c->capacity, c->err, c->sink, *fr);
-        else
-            hipLaunchKernelGGL(zrc4::crypt_half_kernel<false>, hgrid, hblk, 0, s, c->arena, c->xy, first_slot,
-                               payload, off, len, n, c->capacity, c->err, c->sink, zrc4::FrameArgs{});
+        const dim3 hblk(zrc4::kGroup / 2);
+        const dim3 hgrid(mode == zrc4::kGrouped ? 2u * grid : (n + zrc4::kGroup / 2 - 1) / (zrc4::kGroup / 2));
+        const zrc4::FrameArgs fa = fr ? *fr : zrc4::FrameArgs{};
+        if (mode == zrc4::kRange) {
+            if (fr)
+                hipLaunchKernelGGL((zrc4::crypt_half_kernel<zrc4::kRange, true>), hgrid, hblk, 0, s, c->arena, c->xy,
+                                   ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa);
+            else
+                hipLaunchKernelGGL((zrc4::crypt_half_kernel<zrc4::kRange, false>), hgrid, hblk, 0, s, c->arena, c->xy,
+                                   ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa);
+        } else {
+            if (fr)
+                hipLaunchKernelGGL((zrc4::crypt_half_kernel<zrc4::kGrouped, true>), hgrid, hblk, 0, s, c->arena,
+                                   c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa);
+            else
+                hipLaunchKernelGGL((zrc4::crypt_half_kernel<zrc4::kGrouped, false>), hgrid, hblk, 0, s, c->arena,
+                                   c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa);
+        }
         return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
     }
     if (fr && !stream_kernel) {

@@ -669,7 +669,7 @@ __device__ __forceinline__ void issue_image_asm(u32x32 &ilo, u32x32 &ihi, const 
 //   kIds      slot = ids[e], arbitrary: whole iff the 256 ids are exactly
 //             g*256 .. g*256+255 in order, otherwise each lane gathers and
 //             scatters its own 256-byte column (correct, strided).
-// HALF (kRange, first_slot % 256 == 0, few groups): 128-thread workgroups,
+// HALF (kRange with first_slot % 256 == 0, or kGrouped; few groups): 128-thread workgroups,
 // each owning the two waves of a group whose S-boxes share the dwords of one
 // 128-byte half of every image row (col_of: (wave >> 1) picks the half), so
 // each moves a 32 KiB half image.  The workgroup reserves more LDS than it
@@ -740,7 +740,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
            const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
            uint32_t *__restrict__ err, uint8_t *__restrict__ sink, const FrameArgs &fr)
 {
-    static_assert(!HALF || MODE == kRange, "half-group workgroups are range batches");
+    static_assert(!HALF || MODE != kIds, "half-group workgroups run range and grouped batches");
     __shared__ __attribute__((aligned(16))) uint8_t smem[HALF ? kSmemHalf : kSmemDirect];
     uint8_t *S = smem;
     if (!lds_base_ok(S, err)) return;
@@ -776,43 +776,72 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         slot = valid ? first_slot + e : ZRC4_INVALID;
         sxy = valid ? xy[slot] : (uint16_t)0;
     } else if constexpr (MODE == kGrouped) {
-        // 1. this thread's entry; 2. the bucket's group (min and max group of
-        //    its busy entries must agree) and the slot -> entry table; 3. lane
-        //    j takes the entry of slot g*256 + j.
+        // 1. the bucket's entries (HALF: both halves read all 256, each
+        //    thread kPer of them); 2. its group (every busy entry must name
+        //    the same one: checked per wave against the wave's guess, then
+        //    across waves by one atomic min/max per wave) and the slot ->
+        //    entry table; 3. lane j takes the entry of slot g*256 + j.
+        constexpr uint32_t kPer = kGroup / kLanes;
+        const uint32_t w = HALF ? blockIdx.x >> 1 : blockIdx.x;
         uint32_t *te = reinterpret_cast<uint32_t *>(smem + kTabOff);          // entry index
         uint32_t *tl = te + 256;                                              // length
         uint64_t *to = reinterpret_cast<uint64_t *>(smem + kTabOff + 2048);   // offset
-        uint32_t id = valid ? ids[e] : ZRC4_INVALID;
-        const uint32_t elen = valid ? len[e] : 0u;
-        const uint64_t eoff = valid ? off[e] : 0u;
-        if (valid && id >= capacity && id != ZRC4_INVALID) {    // ZRC4_IDLE_SLOT pads buckets
-            latch_fault(err, kErrSlotRange);
-            id = ZRC4_INVALID;
+        uint32_t idq[kPer], lq[kPer];
+        uint64_t oq[kPer];
+        bool bq[kPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+            const uint32_t eq = w * kGroup + q * kLanes + tid;
+            const bool vq = eq < n;
+            uint32_t id = vq ? ids[eq] : ZRC4_INVALID;
+            lq[q] = vq ? len[eq] : 0u;
+            oq[q] = vq ? off[eq] : 0u;
+            if (vq && id >= capacity && id != ZRC4_INVALID) {   // ZRC4_IDLE_SLOT pads buckets
+                latch_fault(err, kErrSlotRange);
+                id = ZRC4_INVALID;
+            }
+            idq[q] = id;
+            bq[q] = id != ZRC4_INVALID && lq[q] != 0u;
         }
-        const bool busy = id != ZRC4_INVALID && elen != 0u;
-        // Speculative image (and x/y) issue: every busy entry of a wave must
-        // lie in the bucket's group, so the wave's first busy id names it and
-        // the image load overlaps the table build below.  A wave with no busy
-        // entry (or a wrong guess: a contract violation, refused below) loads
-        // again once the group is known.
-        const uint64_t bm = __ballot(busy);
-        const uint32_t gw = bm ? (__builtin_amdgcn_readlane(id, (int)__builtin_ctzll(bm)) >> 8) : 0u;
+        // Speculative image (and x/y) issue: the wave's first busy id names
+        // the bucket's group, so the image load overlaps the table build.  A
+        // wave with no busy entry (or a wrong guess: a contract violation,
+        // refused below) loads again once the group is known.
+        bool have = false;
+        uint32_t gw = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+            const uint64_t bm = __ballot(bq[q]);
+            if (!have && bm) {
+                gw = __builtin_amdgcn_readlane(idq[q], (int)__builtin_ctzll(bm)) >> 8;
+                have = true;
+            }
+        }
         issue_image_asm(ilo, ihi, arena + (size_t)gw * kGroupBytes, vo0);
         const uint16_t xyw = xy[gw * 256u + j];
-        te[tid] = ZRC4_INVALID;
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) te[q * kLanes + tid] = ZRC4_INVALID;
         if (tid == 0) {
             flag[0] = 0xFFFFFFFFu;
             flag[1] = 0u;
             flag[2] = 0u;
         }
         __syncthreads();
-        if (busy) {
-            atomicMin(const_cast<uint32_t *>(flag), id >> 8);
-            atomicMax(const_cast<uint32_t *>(flag + 1), id >> 8);
-            if (atomicExch(&te[id & 255u], e) != ZRC4_INVALID) flag[2] = 1u;   // a slot twice
-            tl[id & 255u] = elen;
-            to[id & 255u] = eoff;
+        if (have && (tid & 63u) == 0u) {
+            atomicMin(const_cast<uint32_t *>(flag), gw);
+            atomicMax(const_cast<uint32_t *>(flag + 1), gw);
         }
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+            if (bq[q]) {
+                const uint32_t k = idq[q] & 255u;
+                if ((idq[q] >> 8) != gw) flag[2] = 1u;                                  // another group
+                if (atomicExch(&te[k], w * kGroup + q * kLanes + tid) != ZRC4_INVALID) flag[2] = 1u;   // a slot twice
+                tl[k] = lq[q];
+                to[k] = oq[q];
+            }
+        }
+        const bool busy = bq[HALF ? h : 0u];             // this thread's own entry e
         __syncthreads();
         const uint32_t gmin = flag[0], gmax = flag[1], dup = flag[2];
         if (gmin == 0xFFFFFFFFu || gmin != gmax || dup) {
@@ -831,7 +860,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         myoff = ent != ZRC4_INVALID ? to[j] : 0u;
         slot = g * 256u + j;
         sxy = xyw;
-        if (!bm || gw != g) {                            // wave-uniform: the guess missed
+        if (!have || gw != g) {                          // wave-uniform: the guess missed
             asm volatile("s_waitcnt vmcnt(0)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
             issue_image_asm(ilo, ihi, arena + (size_t)g * kGroupBytes, vo0);
             sxy = xy[slot];
@@ -944,15 +973,17 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     crypt_body<MODE, FRAME, false>(arena, xy, ids, first_slot, payload, off, len, n, capacity, err, sink, fr);
 }
 
-// Half-group workgroups (kRange, few groups): 128 threads, one per CU.
-template <bool FRAME = false>
+// Half-group workgroups (kRange / kGrouped, few groups): 128 threads, one per
+// CU; workgroup 2w + h runs half h of bucket w.
+template <int MODE, bool FRAME = false>
 __global__ void __launch_bounds__(128, 1)
-crypt_half_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uint32_t first_slot,
+crypt_half_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
+                  const uint32_t *__restrict__ ids, uint32_t first_slot,
                   uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
                   const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
                   uint32_t *__restrict__ err, uint8_t *__restrict__ sink, FrameArgs fr = FrameArgs{})
 {
-    crypt_body<kRange, FRAME, true>(arena, xy, nullptr, first_slot, payload, off, len, n, capacity, err, sink, fr);
+    crypt_body<MODE, FRAME, true>(arena, xy, ids, first_slot, payload, off, len, n, capacity, err, sink, fr);
 }
 
 // ---------------------------------------------------------------------------
