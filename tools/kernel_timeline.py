@@ -45,12 +45,49 @@ def summarise(rec: np.ndarray, waves: int, L: int) -> dict:
             "chain_cyc_per_byte": q((c[:, 2] - c[:, 1]) / max(L, 1))}
 
 
+def placement(rec: np.ndarray, hwid: np.ndarray, act: np.ndarray, L: int) -> dict:
+    """gfx9 HW_ID fields (wave 3:0, simd 5:4, cu 11:8, sh 12, se 15:13) + XCC_ID;
+    chain cycles/byte per wave, and the same split by how many active waves
+    ran on the wave's CU, its CU pair (cu >> 1) and its SIMD."""
+    c = rec[:, 4:].astype(np.float64)
+    cyc = (c[:, 2] - c[:, 1]) / max(L, 1)
+    h = hwid[:, 0]
+    simd, cu, sh, se = (h >> 4) & 3, (h >> 8) & 15, (h >> 12) & 1, (h >> 13) & 7
+    xcc = hwid[:, 1] & 15
+    key_cu = [(int(x), int(a), int(b), int(u)) for x, a, b, u in zip(xcc, se, sh, cu)]
+    key_pair = [(k[0], k[1], k[2], k[3] >> 1) for k in key_cu]
+    key_simd = [k + (int(sd),) for k, sd in zip(key_cu, simd)]
+    from collections import Counter
+    n_cu = Counter(k for k, a in zip(key_cu, act) if a)
+    n_pair = Counter(k for k, a in zip(key_pair, act) if a)
+    n_simd = Counter(k for k, a in zip(key_simd, act) if a)
+    out = {"by_waves_on_cu": {}, "by_waves_on_cu_pair": {}, "by_waves_on_simd": {}, "slow": []}
+    med = float(np.median(cyc[act]))
+    for name, keys, cnt in (("by_waves_on_cu", key_cu, n_cu), ("by_waves_on_cu_pair", key_pair, n_pair),
+                            ("by_waves_on_simd", key_simd, n_simd)):
+        groups = {}
+        for i in np.flatnonzero(act):
+            groups.setdefault(cnt[keys[i]], []).append(cyc[i])
+        out[name] = {str(k): {"waves": len(v), "med": round(float(np.median(v)), 2), "max": round(float(max(v)), 2)}
+                     for k, v in sorted(groups.items())}
+    for i in np.flatnonzero(act):
+        if cyc[i] > med + 2:
+            out["slow"].append({"wave": int(i), "cyc": round(float(cyc[i]), 2), "xcc": int(xcc[i]), "se": int(se[i]),
+                                "sh": int(sh[i]), "cu": int(cu[i]), "simd": int(simd[i])})
+    out["slow"] = out["slow"][:24]
+    out["all"] = [[int(xcc[i]), int(se[i]), int(sh[i]), int(cu[i]), int(simd[i]), round(float(cyc[i]), 1)]
+                  for i in np.flatnonzero(act)][:256]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workloads", default="cfg2,cfg3,65536x1024")
     ap.add_argument("--launches", type=int, default=12)
     ap.add_argument("--footprint-mib", type=int, default=640)
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--placement", action="store_true",
+                    help="per-wave chain cycles/byte against where the wave ran (XCC, SE, SH, CU, SIMD)")
     ap.add_argument("--ids", choices=("range", "grouped"), default="range",
                     help="grouped: slots permuted inside each group, groups in random order (bench.py --ids grouped) "
                          "through zrc4_crypt_grouped")
@@ -124,11 +161,17 @@ def main():
         rc = hip.hipMemcpy(C.c_void_p(rec.ctypes.data), sink, C.c_size_t(rec.nbytes), 2)
         if rc:
             raise SystemExit(f"hipMemcpy failed {rc}")
+        hwid = np.zeros((1024, 2), dtype=np.uint32)
+        rc = hip.hipMemcpy(C.c_void_p(hwid.ctypes.data), C.c_void_p(sink.value + 65536), C.c_size_t(hwid.nbytes), 2)
+        if rc:
+            raise SystemExit(f"hipMemcpy failed {rc}")
         waves = (S + 63) // 64
         act = np.array([(w % 4) < args.active_waves for w in range(waves)])
         out[wl] = summarise(rec[:waves][act], int(act.sum()), L)
         out[wl]["active_waves_per_group"] = args.active_waves
         out[wl]["ids"] = args.ids
+        if args.placement:
+            print(wl, "placement:", json.dumps(placement(rec[:waves], hwid[:waves], act, L)), flush=True)
         print(wl, json.dumps(out[wl]), flush=True)
         lib.zrc4_destroy(h)
         del keys, adv, pay, off, ids, ln, klen, koff, zoff

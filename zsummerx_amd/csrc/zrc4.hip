@@ -96,7 +96,7 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
     const bool half = ZRC4_HALF && 2u * grid <= (uint32_t)c->num_cus &&
                       ((mode == zrc4::kRange && (first_slot & 255u) == 0u) || mode == zrc4::kGrouped);
     if (half) {
-        const dim3 hblk(zrc4::kGroup / 2);
+        const dim3 hblk(zrc4::kHalfBlock);
         const dim3 hgrid(mode == zrc4::kGrouped ? 2u * grid : (n + zrc4::kGroup / 2 - 1) / (zrc4::kGroup / 2));
         const zrc4::FrameArgs fa = fr ? *fr : zrc4::FrameArgs{};
         if (mode == zrc4::kRange) {

@@ -89,15 +89,24 @@ __device__ __forceinline__ void stamp(Stamps &s, int i)
     s.c[i] = __builtin_amdgcn_s_memtime();
 #endif
 }
-__device__ __forceinline__ void stamps_out(const Stamps &s, uint8_t *sink)
+// `wave`: the wave's index in batch-entry order (entry >> 6).
+__device__ __forceinline__ void stamps_out(const Stamps &s, uint8_t *sink, uint32_t wave)
 {
 #if ZRC4_TIMING
     if ((threadIdx.x & 63u) == 0u) {
-        uint64_t *o = reinterpret_cast<uint64_t *>(sink + ((((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & 1023u) * 64u));
+        uint64_t *o = reinterpret_cast<uint64_t *>(sink + ((wave & 1023u) * 64u));
         for (int i = 0; i < 4; ++i) {
             o[i] = s.r[i];
             o[4 + i] = s.c[i];
         }
+        // where the wave ran: HW_ID (wave/simd/cu/sh/se fields) and XCC_ID,
+        // after the 64 KiB of stamps (the timing build's sink is larger)
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
+                     : "=s"(hw), "=s"(xcc));
+        uint32_t *w = reinterpret_cast<uint32_t *>(sink + 65536u + (wave & 1023u) * 8u);
+        w[0] = hw;
+        w[1] = xcc;
     }
 #endif
 }
@@ -472,7 +481,8 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #include "zrc4_line_loop.inc"
 
 constexpr uint32_t kSinkSlot = 256;                 // bytes of sink per thread (128-B line + offsets)
-constexpr uint32_t kSinkBytes = kGroup * kSinkSlot; // one 64 KiB sink per context, shared by all workgroups
+constexpr uint32_t kSinkBytes = kGroup * kSinkSlot  // one 64 KiB sink per context, shared by all workgroups
+                                + (ZRC4_TIMING ? 8192u : 0u);   // + where each timed wave ran
 
 // line = blocks at b0 (16 B x 4) and b1 (16 B x 4)
 __device__ __forceinline__ void preload_line(u32x32 &v, const uint8_t *b0, const uint8_t *b1)
@@ -728,6 +738,9 @@ __device__ __forceinline__ void frame_walk(const uint8_t *b, uint32_t L, uint32_
 // addresses), then 16 B of flags, then the kGrouped entry table (slot -> entry
 // index / length / offset).  HALF pads the allocation past 80 KiB so that a
 // CU holds one workgroup.
+#ifndef ZRC4_HALF_PAD
+#define ZRC4_HALF_PAD 1
+#endif
 constexpr uint32_t kTabOff = kGroupBytes + 16;
 constexpr uint32_t kSmemDirect = kTabOff + 256 * 16;          // 69 648 B: two workgroups per CU
 constexpr uint32_t kSmemHalf = 96 * 1024;                     // one workgroup per CU
@@ -748,7 +761,35 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     stamp(ts, 0);
 
     constexpr uint32_t kLanes = HALF ? 128u : 256u;
-    const uint32_t tid = threadIdx.x;
+    uint32_t tid = threadIdx.x;
+    if constexpr (HALF && ZRC4_HALF_PAD) {
+        // The workgroup has 4 waves; the two that work are the ones on SIMDs
+        // 1 and 2 (else 1 and 3).  Measured per wave (in-kernel clocks,
+        // tools/kernel_timeline.py --placement, profiles/r02/placement_*.log):
+        // a lone wave runs the step at 96 cycles/byte on SIMDs 1-3 and 100 on
+        // SIMD 0; a pair runs at 96 only when one of them is on SIMD 1
+        // ({2,3}, {0,2}, {0,3} pairs: 100).  The other two waves end here.
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        uint32_t *sid = reinterpret_cast<uint32_t *>(smem + kSmemDirect);
+        const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        if ((threadIdx.x & 63u) == 0u) sid[w] = (hw >> 4) & 3u;
+        __syncthreads();
+        uint32_t ss[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ss[i] = __builtin_amdgcn_readfirstlane(sid[i]);
+        uint32_t a = 4u, b = 4u, c = 4u;
+#pragma unroll
+        for (uint32_t i = 0; i < 4u; ++i) {
+            if (a == 4u && ss[i] == 1u) a = i;
+            if (b == 4u && ss[i] == 2u) b = i;
+            if (c == 4u && ss[i] == 3u) c = i;
+        }
+        if (b == 4u) b = c;
+        if (a == 4u || b == 4u) { a = 0u; b = 1u; }      // waves not one per SIMD: the first two
+        if (w != a && w != b) return;                    // uniform (SGPR) branch: the wave ends
+        tid = (w == a ? 0u : 64u) + (threadIdx.x & 63u);
+    }
     const uint32_t e = blockIdx.x * kLanes + tid;        // batch entry of this thread
     const bool valid = e < n;
     const uint32_t h = HALF ? (blockIdx.x & 1u) : 0u;    // half of the group (HALF)
@@ -958,7 +999,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #if ZRC4_TIMING
     __builtin_amdgcn_s_waitcnt(0);
     stamp(ts, 3);
-    stamps_out(ts, sink);
+    stamps_out(ts, sink, e >> 6);
 #endif
 }
 
@@ -973,10 +1014,14 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     crypt_body<MODE, FRAME, false>(arena, xy, ids, first_slot, payload, off, len, n, capacity, err, sink, fr);
 }
 
-// Half-group workgroups (kRange / kGrouped, few groups): 128 threads, one per
-// CU; workgroup 2w + h runs half h of bucket w.
+// Half-group workgroups (kRange / kGrouped, few groups): one per CU;
+// workgroup 2w + h runs half h of bucket w.  ZRC4_HALF_PAD: launched with 256
+// threads, of which the two waves that work are picked by SIMD (crypt_body);
+// A/B knob: 0 launches 128 threads.
+constexpr uint32_t kHalfBlock = ZRC4_HALF_PAD ? 256u : 128u;
+
 template <int MODE, bool FRAME = false>
-__global__ void __launch_bounds__(128, 1)
+__global__ void __launch_bounds__(kHalfBlock, 1)
 crypt_half_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                   const uint32_t *__restrict__ ids, uint32_t first_slot,
                   uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
