@@ -6,7 +6,9 @@ crypt_message_dpp, for the C++ side and the register contract).
 One iteration ("half") handles one 128-byte line per lane (blocks b, b+1 of
 the lane's own session):
   1. wait for the line's loads (counted vmcnt: every VMEM op of the loop is
-     issued with the full exec mask, so the counts are static);
+     issued with the full exec mask, so the counts are static; the first
+     half is entered past this wait, at LL_PSTART: its line is retired by the
+     caller and the second line is still in flight);
   2. RC4 keystream XOR over the two 64-byte blocks (ZL_BLOCK, exec = lanes
      whose session has that block);
   3. 8x8 transpose of 16-byte chunks inside each group of 8 consecutive lanes
@@ -37,6 +39,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 OUT = ROOT / "zsummerx_amd" / "csrc" / "zrc4_line_loop.inc"
+OUT_AB = ROOT / "zsummerx_amd" / "csrc" / "ab" / "zrc4_line_loop_ab.inc"
 
 P_BASE, Q_BASE, X_BASE = 40, 72, 104      # 8 + 8 + 4 tuples of 4 VGPRs
 ADDR_BASE = 120                            # 8 x 64-bit store addresses (chunk i of session 8g+q)
@@ -120,7 +123,12 @@ def zl_block(base: int) -> str:
     return "ZL_BLOCK(" + ", ".join(f"v{base + d}" for d in range(16)) + ")"
 
 
-def half(name: str, cur: int) -> str:
+def half(name: str, cur: int, ab: int = 0) -> str:
+    """ab (timing-only A/B builds, zrc4_line_loop_ab.inc; outputs are wrong):
+    1 stores to the lane's sink slot (one 64 KiB sink for the whole chip:
+    contended), 2 loads from it, 3 no transpose, 4 both sinks, 5 no stores (a
+    sink load in place of each, so the vmcnt counts hold), 6 = 5 + loads from
+    the sink."""
     start = {c: cur + 4 * c for c in range(8)}
     tl, final, ops, _ = transpose_plan(start, [X_BASE + 4 * t for t in range(4)])
     simulate(ops, start, final)
@@ -138,6 +146,10 @@ def half(name: str, cur: int) -> str:
     w(q("s_waitcnt vmcnt(8)"))
     w(q(f"LL_{name}W_%=:"))
     w(q("s_waitcnt vmcnt(20)"))
+    if name == "P":
+        # entry of the first half: line 0 (P) was retired by the caller and
+        # line 1 (Q) may still be in flight (issued after the S-box fill)
+        w(q("LL_PSTART_%=:"))
     w(q("v_cmp_lt_u32_e64 %[msk], %[sb], %[nblk]"))
     w(q("s_and_b64 exec, %[full], %[msk]"))
     w(q(f"s_cbranch_execz LL_{name}1_%="))
@@ -153,8 +165,11 @@ def half(name: str, cur: int) -> str:
     w(q("s_mov_b64 exec, %[full]"))
     w(q("s_nop 4"))                                    # exec write -> DPP
     # 3. transpose
-    for line in tl:
-        w(q(line))
+    if ab != 3:
+        for line in tl:
+            w(q(line))
+    else:
+        final = dict(start)
     # 4. stores: chunk i of session 8g+q's line, or the sink past its last block
     for qq in range(8):
         sa = SA0 if qq % 2 == 0 else SA1
@@ -162,7 +177,12 @@ def half(name: str, cur: int) -> str:
         w(q(f"v_cmp_gt_u32_e64 %[msk], v{LIM_BASE + qq}, %[sb]"))
         w(q(f"v_cndmask_b32_e64 v{sa}, v{SINK}, v{a}, %[msk]"))
         w(q(f"v_cndmask_b32_e64 v{sa + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
-        w(f'"global_store_dwordx4 v[{sa}:{sa + 1}], v[{final[qq]}:{final[qq] + 3}], off nt\\n\\t"')
+        if ab in (1, 4):
+            sa = SINK
+        if ab in (5, 6):     # no store: a sink load keeps the vmcnt counts
+            w(f'"global_load_dword v{sa}, v[{SINK}:{SINK + 1}], off\\n\\t"')
+        else:
+            w(f'"global_store_dwordx4 v[{sa}:{sa + 1}], v[{final[qq]}:{final[qq] + 3}], off nt\\n\\t"')
     for qq in range(8):
         a = ADDR_BASE + 2 * qq
         w(q(f"v_lshl_add_u64 v[{a}:{a + 1}], 8, 4, v[{a}:{a + 1}]"))     # += 8 << 4 (shift must be 0..4)
@@ -174,14 +194,16 @@ def half(name: str, cur: int) -> str:
     w(q("v_cmp_lt_u32_e64 %[msk], %[s1], %[nblk]"))
     w(q(f"v_cndmask_b32_e64 v{LA}, v{SINK}, %[palo], %[msk]"))
     w(q(f"v_cndmask_b32_e64 v{LA + 1}, v{SINK + 1}, %[pahi], %[msk]"))
+    la = SINK if ab in (2, 4, 6) else LA
+    lb = SINK if ab in (2, 4, 6) else LB
     for d in range(4):
-        w(f'"global_load_dwordx4 v[{cur + 4 * d}:{cur + 4 * d + 3}], v[{LA}:{LA + 1}], off offset:{16 * d}\\n\\t"')
+        w(f'"global_load_dwordx4 v[{cur + 4 * d}:{cur + 4 * d + 3}], v[{la}:{la + 1}], off offset:{16 * d}\\n\\t"')
     w(q("s_add_u32 %[s1], %[sb], 5"))
     w(q("v_cmp_lt_u32_e64 %[msk], %[s1], %[nblk]"))
     w(q(f"v_cndmask_b32_e64 v{LB}, v{SINK}, %[palo], %[msk]"))
     w(q(f"v_cndmask_b32_e64 v{LB + 1}, v{SINK + 1}, %[pahi], %[msk]"))
     for d in range(4):
-        w(f'"global_load_dwordx4 v[{cur + 16 + 4 * d}:{cur + 16 + 4 * d + 3}], v[{LB}:{LB + 1}], off offset:{64 + 16 * d}\\n\\t"')
+        w(f'"global_load_dwordx4 v[{cur + 16 + 4 * d}:{cur + 16 + 4 * d + 3}], v[{lb}:{lb + 1}], off offset:{64 + 16 * d}\\n\\t"')
     w(q("v_add_co_u32_e32 %[palo], vcc, 0x80, %[palo]"))
     w(q("v_addc_co_u32_e32 %[pahi], vcc, 0, %[pahi], vcc"))
     w(q(f"LL_{name}L_%=:"))
@@ -217,6 +239,15 @@ def main():
     ]
     OUT.write_text("".join(text))
     print("wrote", OUT)
+    ab = ["// GENERATED by tools/gen_line_loop.py -- do not edit by hand.\n",
+          "// Timing-only A/B variants of zrc4_line_loop.inc (outputs are WRONG), selected by\n",
+          "// ZRC4_LL_AB: 1 stores to the sink, 2 loads from the sink, 3 no transpose, 4 both sinks,\n",
+          "// 5 no stores, 6 no stores + loads from the sink.\n",
+          "#pragma once\n"]
+    for v in (1, 2, 3, 4, 5, 6):
+        ab += [f"#if ZRC4_LL_AB == {v}\n", half("P", P_BASE, v), half("Q", Q_BASE, v), "#endif\n"]
+    OUT_AB.write_text("".join(ab))
+    print("wrote", OUT_AB)
 
 
 if __name__ == "__main__":

@@ -89,6 +89,29 @@ __device__ __forceinline__ void stamp(Stamps &s, int i)
     s.c[i] = __builtin_amdgcn_s_memtime();
 #endif
 }
+// crypt_stream_kernel (ZRC4_TIMING): lane 0 of workgroup wg's wave 0 stamps
+// event i (0 entry, 1 + 2k / 2 + 2k group k's keystream start / end, 15 exit)
+// as s_memrealtime into sink[wg * 16 + i] (512 workgroups); entry and exit
+// shader clocks go to sink + 64 KiB, HW_ID / XCC_ID to sink + 72 KiB.
+__device__ __forceinline__ void stream_stamp(uint8_t *sink, uint32_t i)
+{
+#if ZRC4_TIMING
+    if (threadIdx.x == 0u && blockIdx.x < 512u && i < 16u) {
+        reinterpret_cast<uint64_t *>(sink)[blockIdx.x * 16u + i] = __builtin_amdgcn_s_memrealtime();
+        if (i == 0u || i == 15u)
+            reinterpret_cast<uint64_t *>(sink + 65536u)[blockIdx.x * 2u + (i ? 1u : 0u)] = __builtin_amdgcn_s_memtime();
+        if (i == 0u) {
+            uint32_t hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
+                         : "=s"(hw), "=s"(xcc));
+            uint32_t *o = reinterpret_cast<uint32_t *>(sink + 65536u + 8192u) + blockIdx.x * 2u;
+            o[0] = hw;
+            o[1] = xcc;
+        }
+    }
+#endif
+}
+
 // `wave`: the wave's index in batch-entry order (entry >> 6).
 __device__ __forceinline__ void stamps_out(const Stamps &s, uint8_t *sink, uint32_t wave)
 {
@@ -471,18 +494,23 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 //   * stores (nt): chunk i of the line of session 8g+q from lane 8g+i, or the
 //     sink past that session's last block (ragged batches);
 //   * exec is narrowed only around the keystream of each 64-byte block.
-// The caller preloads lines 0 and 1 (P, Q) before the S-box image fill.
+// The caller loads line 0 (P) before the S-box image fill and issues line 1
+// (Q) after it (issue_line1_asm); the loop's first half skips its wait.
 // ---------------------------------------------------------------------------
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+#if defined(ZRC4_LL_AB) && ZRC4_LL_AB
+#include "ab/zrc4_line_loop_ab.inc"   // timing-only A/B builds (tools/ab_bench.py --no-check)
+#else
 #include "zrc4_line_loop.inc"
+#endif
 
 constexpr uint32_t kSinkSlot = 256;                 // bytes of sink per thread (128-B line + offsets)
 constexpr uint32_t kSinkBytes = kGroup * kSinkSlot  // one 64 KiB sink per context, shared by all workgroups
-                                + (ZRC4_TIMING ? 8192u : 0u);   // + where each timed wave ran
+                                + (ZRC4_TIMING ? 16384u : 0u);  // + where each timed wave ran / stream clocks and ids
 
 // line = blocks at b0 (16 B x 4) and b1 (16 B x 4)
 __device__ __forceinline__ void preload_line(u32x32 &v, const uint8_t *b0, const uint8_t *b1)
@@ -537,13 +565,37 @@ __device__ __forceinline__ void line_roles(u32x16 &addr, u32x8 &lim, const LineS
     }
 }
 
-// Lines 0 and 1 (the lane's own blocks 0..3; the sink past the session's end).
-__device__ __forceinline__ void preload_lines(u32x32 &P, u32x32 &Q, const LineSetup &ls, const uint8_t *sk)
+// Line 0 (the lane's own blocks 0, 1; the sink past the session's end): the
+// compiler's loads, retired before the S-box fill.
+__device__ __forceinline__ void preload_line0(u32x32 &P, const LineSetup &ls, const uint8_t *sk)
 {
     const uint8_t *p = reinterpret_cast<const uint8_t *>((uintptr_t)ls.p);
     const uint32_t nb = ls.nblk;
     preload_line(P, nb > 0 ? p : sk, nb > 1 ? p + 64 : sk + 64);
-    preload_line(Q, nb > 2 ? p + 128 : sk, nb > 3 ? p + 192 : sk + 64);
+}
+
+// Line 1 (blocks 2, 3), issued from asm after the S-box fill, so it is in
+// flight while line 0's keystream runs (the loop's first half is entered past
+// its wait; the second half's counted wait retires it).  Only when the wave
+// has a second line (wmax > 2): otherwise no half would wait for these
+// registers before the compiler reuses them.
+__device__ __forceinline__ void issue_line1_asm(u32x32 &Q, const LineSetup &ls, const uint8_t *sk)
+{
+    const uint8_t *p = reinterpret_cast<const uint8_t *>((uintptr_t)ls.p);
+    const uint32_t nb = ls.nblk;
+    const uint8_t *b0 = nb > 2 ? p + 128 : sk, *b1 = nb > 3 ? p + 192 : sk + 64;
+    asm volatile(
+        "global_load_dwordx4 v[72:75], %[a0], off\n\t"
+        "global_load_dwordx4 v[76:79], %[a0], off offset:16\n\t"
+        "global_load_dwordx4 v[80:83], %[a0], off offset:32\n\t"
+        "global_load_dwordx4 v[84:87], %[a0], off offset:48\n\t"
+        "global_load_dwordx4 v[88:91], %[a1], off\n\t"
+        "global_load_dwordx4 v[92:95], %[a1], off offset:16\n\t"
+        "global_load_dwordx4 v[96:99], %[a1], off offset:32\n\t"
+        "global_load_dwordx4 v[100:103], %[a1], off offset:48\n\t"
+        : "=&{v[72:103]}"(Q)
+        : [a0] "v"(b0), [a1] "v"(b1)
+        : "memory");
 }
 
 __device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls,
@@ -558,6 +610,7 @@ __device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &
     asm volatile(
         "s_mov_b64 %[full], exec\n\t"
         "s_mov_b32 %[sb], 0\n\t"
+        "s_branch LL_PSTART_%=\n\t"
         "LL_LOOP_%=:\n\t"
         ZRC4_LL_HALF_P
         ZRC4_LL_HALF_Q
@@ -1044,7 +1097,10 @@ crypt_half_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 // in VGPRs), its batch entries and -- once the message loop is done -- its
 // first two payload lines are already in flight, and the finished image goes
 // back to HBM behind the next group's work.  At a boundary only the LDS
-// copies and three barriers remain.
+// copies and three barriers remain.  Only line 0 of a group is loaded before
+// its S-box fill; line 1 goes out behind the fill (profiles/r02/stream_tl_*:
+// the launch prologue, every workgroup loading its image and first lines at
+// once, was 12-18 us).
 //   PF = range batch with first_slot % 256 == 0: every group is a whole,
 //        aligned image and is prefetched; otherwise (ids, unaligned range)
 //        each group decides whole/gather as crypt_kernel<kIds> does,
@@ -1082,8 +1138,8 @@ __device__ __forceinline__ void load_entry(EntryIn &d, uint32_t w, const uint32_
 // through so the compiler's wait for this group's first lines lands BEFORE
 // these loads.  Consumers wait explicitly:
 //   entries  "s_waitcnt vmcnt(16)" (the 16 image loads are younger);
-//   image    "s_waitcnt vmcnt(32)" (the next lines' 16 loads and this image's
-//            16 stores are younger).
+//   image    "s_waitcnt vmcnt(24)" (the next group's line-0 loads (8) and
+//            this image's 16 stores are younger).
 __device__ __forceinline__ void prefetch_group(u32x32 &P, u32x32 &Q, u32x32 &ilo, u32x32 &ihi,
                                                uint32_t &rlen, uint64_t &roff, uint32_t &rxy,
                                                const uint32_t *alen, const uint64_t *aoff,
@@ -1147,6 +1203,8 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     const uint32_t col = col_of(j);
     const uint32_t nwg = (n + kGroup - 1) / kGroup;
     uint8_t *sk = sink + (size_t)j * kSinkSlot;
+    stream_stamp(sink, 0);
+    uint32_t k_t = 0;                         // groups done (ZRC4_TIMING stamps)
 
     uint32_t w = blockIdx.x;
     EntryIn cur;
@@ -1166,13 +1224,13 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     }
     LineSetup ls;
     line_setup(ls, payload + cur.off, cur.len);
-    u32x32 P, Q;
-    preload_lines(P, Q, ls, sk);
+    u32x32 P, Q = {};
+    preload_line0(P, ls, sk);
     // Retire the prologue's loads here, once: inside the loop the compiler's
     // waitcnt analysis merges the first iteration with the back edge, and a
     // value still pending from the prologue would put a vmcnt(0) -- draining
     // the asm prefetch -- into every iteration.
-    asm volatile("" : "+v"(cur.len), "+v"(cur.off), "+v"(cur.xy), "+{v[40:71]}"(P), "+{v[72:103]}"(Q),
+    asm volatile("" : "+v"(cur.len), "+v"(cur.off), "+v"(cur.xy), "+{v[40:71]}"(P),
                  "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi));
 
     for (;;) {
@@ -1183,7 +1241,9 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         if constexpr (PF) {
             whole = true;
             g = (first_slot >> 8) + w;
-            asm volatile("s_waitcnt vmcnt(32)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
+            // younger than the prefetched image: at least the next group's
+            // line-0 loads (8) and this image's stores (16)
+            asm volatile("s_waitcnt vmcnt(24)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
             u32x4 *dst = reinterpret_cast<u32x4 *>(S);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -1221,10 +1281,12 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         uint32_t rlen = 0, rxy = 0;
         uint64_t roff = 0;
         uint32_t en = 0;
-        // This group's first lines are needed now (compiler wait: vmcnt(16),
-        // the previous image's stores are younger); past this point they are
-        // asm-defined, so nothing the compiler tracks is pending at the loop.
-        asm volatile("" : "+{v[40:71]}"(P), "+{v[72:103]}"(Q));
+        // This group's line 0 is needed now (compiler wait; the previous
+        // image's stores are younger); past this point it is asm-defined, so
+        // nothing the compiler tracks is pending at the loop.  Line 1 goes out
+        // now, behind the fill, and is waited for inside the loop.
+        asm volatile("" : "+{v[40:71]}"(P));
+        if (ls.wmax > 2u) issue_line1_asm(Q, ls, sk);
         if constexpr (PF) {
             if (more) {
                 en = wn * kGroup + j;
@@ -1235,12 +1297,15 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         }
 
         // ---- keystream over this group's messages
+        stream_stamp(sink, 1u + 2u * k_t);
         {
             Rc4Lane st;
             lane_init(st, S, col, cur.xy);
             crypt_message_dpp(S, st, payload + cur.off, cur.len, P, Q, ls, sk);
             if (active && cur.len) xy[cur.slot] = lane_xy(st);
         }
+        stream_stamp(sink, 2u + 2u * k_t);
+        ++k_t;
 
         EntryIn nxt = {0u, ZRC4_INVALID, 0u, 0u};
         if (more) {
@@ -1256,7 +1321,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             }
             // the loop's last two halves issue no loads, so P/Q are free again
             line_setup(ls, payload + nxt.off, nxt.len);
-            preload_lines(P, Q, ls, sk);
+            preload_line0(P, ls, sk);
         }
 
         // ---- this group's state back to HBM
@@ -1271,6 +1336,10 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         cur = nxt;
         w = wn;
     }
+#if ZRC4_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    stream_stamp(sink, 15);
+#endif
 }
 
 // ---------------------------------------------------------------------------
