@@ -78,7 +78,8 @@ def by_place(rt: np.ndarray, hwid: np.ndarray, wgs: int, K: int) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workloads", default="cfg5,131072x1024")
-    ap.add_argument("--launches", type=int, default=12)
+    ap.add_argument("--launches", type=int, default=150,
+                    help="launches before the recorded one: the clock dips for ~30 cfg5 launches and recovers by ~100 (profiles/r02/cfg5_launch_durations.json)")
     ap.add_argument("--footprint-mib", type=int, default=1200)
     ap.add_argument("--build-only", action="store_true")
     args = ap.parse_args()
@@ -109,12 +110,18 @@ def main():
         _capi.check(lib.zrc4_create(C.byref(h), 0, n), "create")
         _capi.check(lib.zrc4_ksa_range(h, 0, C.c_void_p(keys.data_ptr()), C.c_void_p(koff.data_ptr()),
                                        C.c_void_p(klen.data_ptr()), n, st))
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for i in range(args.launches):
             b = i % R
+            if i == args.launches - 1:
+                ev0.record()
             _capi.check(lib.zrc4_crypt_range(h, b * S, C.c_void_p(pay.data_ptr()),
                                              C.c_void_p(off.data_ptr() + 8 * b * S),
                                              C.c_void_p(ln.data_ptr() + 4 * b * S), S, st))
+        ev1.record()
         _capi.check(lib.zrc4_sync(h, st))
+        torch.cuda.synchronize()
+        last_event_us = ev0.elapsed_time(ev1) * 1000.0
         sink = C.c_void_p()
         _capi.check(lib.zrc4_debug_sink(h, C.byref(sink)))
         rt = np.zeros((512, 16), dtype=np.uint64)
@@ -127,6 +134,7 @@ def main():
         groups = -(-S // 256)
         wgs = min(groups, 512)
         out[wl] = summarise(rt, clk, wgs, min(7, groups // wgs))
+        out[wl]["last_launch_event_us"] = round(last_event_us, 2)
         out[wl]["by_place"] = by_place(rt, hwid, wgs, min(7, groups // wgs))
         print(wl, json.dumps(out[wl]), flush=True)
         lib.zrc4_destroy(h)

@@ -708,6 +708,7 @@ __device__ __forceinline__ void issue_image_asm(u32x32 &ilo, u32x32 &ihi, const 
         : "memory");
 }
 
+
 // ---------------------------------------------------------------------------
 // crypt_kernel: batched RC4Encryption::encryption, one group (or, HALF, one
 // half group) per workgroup: launches with at most one group per CU, the
@@ -795,7 +796,8 @@ __device__ __forceinline__ void frame_walk(const uint8_t *b, uint32_t L, uint32_
 #define ZRC4_HALF_PAD 1
 #endif
 constexpr uint32_t kTabOff = kGroupBytes + 16;
-constexpr uint32_t kSmemDirect = kTabOff + 256 * 16;          // 69 648 B: two workgroups per CU
+constexpr uint32_t kSidOff = kTabOff + 256 * 16;              // 16 B: the half-group workgroup's SIMD ids
+constexpr uint32_t kSmemDirect = kSidOff + 16;                // 69 664 B: two workgroups per CU
 constexpr uint32_t kSmemHalf = 96 * 1024;                     // one workgroup per CU
 
 template <int MODE, bool FRAME, bool HALF>
@@ -824,7 +826,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         // ({2,3}, {0,2}, {0,3} pairs: 100).  The other two waves end here.
         uint32_t hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        uint32_t *sid = reinterpret_cast<uint32_t *>(smem + kSmemDirect);
+        uint32_t *sid = reinterpret_cast<uint32_t *>(smem + kSidOff);
         const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         if ((threadIdx.x & 63u) == 0u) sid[w] = (hw >> 4) & 3u;
         __syncthreads();
@@ -1113,11 +1115,11 @@ struct EntryIn {
     uint32_t xy;
 };
 
-__device__ __forceinline__ void load_entry(EntryIn &d, uint32_t w, const uint32_t *ids, uint32_t first_slot,
+__device__ __forceinline__ void load_entry(EntryIn &d, uint32_t w, uint32_t j, const uint32_t *ids, uint32_t first_slot,
                                            const uint64_t *off, const uint32_t *len, uint32_t n,
                                            uint32_t capacity, uint32_t *err, const uint16_t *xy)
 {
-    const uint32_t e = w * kGroup + threadIdx.x;
+    const uint32_t e = w * kGroup + j;
     const bool valid = e < n;
     uint32_t slot = valid ? (ids ? ids[e] : first_slot + e) : ZRC4_INVALID;
     if (valid && slot >= capacity) {
@@ -1143,7 +1145,7 @@ __device__ __forceinline__ void load_entry(EntryIn &d, uint32_t w, const uint32_
 __device__ __forceinline__ void prefetch_group(u32x32 &P, u32x32 &Q, u32x32 &ilo, u32x32 &ihi,
                                                uint32_t &rlen, uint64_t &roff, uint32_t &rxy,
                                                const uint32_t *alen, const uint64_t *aoff,
-                                               const uint16_t *axy, const uint8_t *ibase)
+                                               const uint16_t *axy, const uint8_t *ibase, uint32_t j)
 {
     uint32_t vo;
     asm volatile(
@@ -1184,7 +1186,7 @@ __device__ __forceinline__ void prefetch_group(u32x32 &P, u32x32 &Q, u32x32 &ilo
         "global_load_dwordx4 v[220:223], %[vo], %[ib]\n\t"
         : "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[160:191]}"(ilo), "=&{v[192:223]}"(ihi),
           [rlen] "=&v"(rlen), [roff] "=&v"(roff), [rxy] "=&v"(rxy), [vo] "=&v"(vo)
-        : [alen] "v"(alen), [aoff] "v"(aoff), [axy] "v"(axy), [ib] "s"(ibase), [j] "v"(threadIdx.x)
+        : [alen] "v"(alen), [aoff] "v"(aoff), [axy] "v"(axy), [ib] "s"(ibase), [j] "v"(j)
         : "memory");
 }
 
@@ -1208,7 +1210,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 
     uint32_t w = blockIdx.x;
     EntryIn cur;
-    load_entry(cur, w, ids, first_slot, off, len, n, capacity, err, xy);
+    load_entry(cur, w, j, ids, first_slot, off, len, n, capacity, err, xy);
     u32x32 ilo, ihi;                          // PF: this group's image, 16 x 16 B per lane
     if constexpr (PF) {
         const u32x4 *src = reinterpret_cast<const u32x4 *>(arena + (size_t)((first_slot >> 8) + w) * kGroupBytes);
@@ -1292,7 +1294,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                 en = wn * kGroup + j;
                 const uint32_t ec = en < n ? en : n - 1u;          // in-bounds address for idle lanes
                 prefetch_group(P, Q, ilo, ihi, rlen, roff, rxy, len + ec, off + ec, xy + first_slot + ec,
-                               arena + (size_t)((first_slot >> 8) + wn) * kGroupBytes);
+                               arena + (size_t)((first_slot >> 8) + wn) * kGroupBytes, j);
             }
         }
 
@@ -1317,7 +1319,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                 nxt.slot = v ? first_slot + en : ZRC4_INVALID;
                 nxt.xy = v ? rxy : 0u;
             } else {
-                load_entry(nxt, wn, ids, first_slot, off, len, n, capacity, err, xy);
+                load_entry(nxt, wn, j, ids, first_slot, off, len, n, capacity, err, xy);
             }
             // the loop's last two halves issue no loads, so P/Q are free again
             line_setup(ls, payload + nxt.off, nxt.len);
