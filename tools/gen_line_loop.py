@@ -208,7 +208,7 @@ def half(name: str, cur: int, ab: int = 0) -> str:
     w(q("v_addc_co_u32_e32 %[pahi], vcc, 0, %[pahi], vcc"))
     w(q(f"LL_{name}L_%=:"))
     w(q("s_add_u32 %[sb], %[sb], 2"))
-    w(q("s_cmp_ge_u32 %[sb], %[wmax]"))
+    w(q("s_cmp_ge_u32 %[sb], %[wend]"))               # wend = wmax, or 2 less: stop before the last half
     w(q("s_cbranch_scc1 LL_DONE_%="))
     return f"#define ZRC4_LL_HALF_{name} \\\n    " + " \\\n    ".join(out) + "\n"
 

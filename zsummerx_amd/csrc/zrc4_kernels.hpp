@@ -598,14 +598,16 @@ __device__ __forceinline__ void issue_line1_asm(u32x32 &Q, const LineSetup &ls, 
         : "memory");
 }
 
-__device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls,
-                                                u32x16 &addr, const u32x8 &lim, u32x2 sink)
+// The line loop, halves sb = 0, 2, ... until sb >= wend (wend = wmax: the
+// whole message; wmax rounded down to a multiple of 4, minus 2: all but a
+// final Q half, crypt_last_half_asm).  Returns sb.
+__device__ __forceinline__ uint32_t crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls,
+                                                    u32x16 &addr, const u32x8 &lim, u32x2 sink, uint32_t &palo,
+                                                    uint32_t &pahi, uint32_t wend)
 {
     u32x16 X;
     u32x8 T;
     uint32_t b, k0, k1, a1s, sb, s1;
-    const uint64_t pa = ls.p + 256u;                 // per-lane loads: blocks 4, 5 next
-    uint32_t palo = (uint32_t)pa, pahi = (uint32_t)(pa >> 32);
     uint64_t full, msk;
     asm volatile(
         "s_mov_b64 %[full], exec\n\t"
@@ -624,25 +626,115 @@ __device__ __forceinline__ void crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &
           [full] "=&s"(full), [msk] "=&s"(msk),
           "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
           "=&{v[144:151]}"(T)
-        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), "{v[136:143]}"(lim), "{v[152:153]}"(sink)
+        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(wend), "{v[136:143]}"(lim), "{v[152:153]}"(sink)
+        : "memory", "vcc", "scc");
+    return sb;
+}
+
+// The next group's line 0 into P (v40..v71), in asm (ZRC4_NEXT_LINE0):
+//   wait for the next group's entries (vmcnt(24): the youngest 24 VMEM ops
+//   are the line loop's last loads and stores, or -- two halves -- this
+//   group's second image), then per lane, as line_setup / preload_line0 do:
+//   m = payload + off, L = valid ? len : 0, h = head bytes, nb = (L - h) / 64,
+//   block 0 = nb > 0 ? m + h : sink, block 1 = nb > 1 ? m + h + 64 : sink + 64
+//   (v144..v149 are the line loop's temporaries; the sink slot is v152:153).
+#define ZRC4_NEXT_LINE0                                                                          \
+    "s_waitcnt vmcnt(24)\n\t"                                                                    \
+    "v_cmp_ne_u32_e32 vcc, 0, %[nv]\n\t"                                                         \
+    "v_cndmask_b32_e32 %[nb], 0, %[nlen], vcc\n\t"                                               \
+    "v_lshl_add_u64 v[144:145], %[noff], 0, %[pay]\n\t"                                          \
+    "v_sub_u32_e32 %[h], 0, v144\n\t"                                                            \
+    "v_and_b32_e32 %[h], 15, %[h]\n\t"                                                           \
+    "v_min_u32_e32 %[h], %[h], %[nb]\n\t"                                                        \
+    "v_sub_u32_e32 %[nb], %[nb], %[h]\n\t"                                                       \
+    "v_lshrrev_b32_e32 %[nb], 6, %[nb]\n\t"                                                      \
+    "v_add_co_u32_e32 v144, vcc, v144, %[h]\n\t"                                                 \
+    "v_addc_co_u32_e32 v145, vcc, 0, v145, vcc\n\t"                                              \
+    "v_lshl_add_u64 v[146:147], v[144:145], 0, 64\n\t"                                           \
+    "v_lshl_add_u64 v[148:149], v[152:153], 0, 64\n\t"                                           \
+    "v_cmp_lt_u32_e32 vcc, 0, %[nb]\n\t"                                                         \
+    "v_cndmask_b32_e32 v144, v152, v144, vcc\n\t"                                                \
+    "v_cndmask_b32_e32 v145, v153, v145, vcc\n\t"                                                \
+    "v_cmp_lt_u32_e32 vcc, 1, %[nb]\n\t"                                                         \
+    "v_cndmask_b32_e32 v146, v148, v146, vcc\n\t"                                                \
+    "v_cndmask_b32_e32 v147, v149, v147, vcc\n\t"                                                \
+    "global_load_dwordx4 v[40:43], v[144:145], off\n\t"                                          \
+    "global_load_dwordx4 v[44:47], v[144:145], off offset:16\n\t"                                \
+    "global_load_dwordx4 v[48:51], v[144:145], off offset:32\n\t"                                \
+    "global_load_dwordx4 v[52:55], v[144:145], off offset:48\n\t"                                \
+    "global_load_dwordx4 v[56:59], v[146:147], off\n\t"                                          \
+    "global_load_dwordx4 v[60:63], v[146:147], off offset:16\n\t"                                \
+    "global_load_dwordx4 v[64:67], v[146:147], off offset:32\n\t"                                \
+    "global_load_dwordx4 v[68:71], v[146:147], off offset:48\n\t"
+
+// The final Q half of a message with an even number of halves, preceded by
+// the next group's line-0 loads -- in ONE asm statement: compiler code between
+// the line loop and those loads could move the registers of a line still in
+// flight.  The loads are younger than this half's line, so its counted waits
+// never wait for them, and they have a whole half to land: the statement ends
+// waiting for them, so P leaves it as an ordinary value (the compiler moves
+// registers freely across the group boundary).
+// nlen / noff: the next group's prefetched entry registers themselves (in
+// flight until the wait; "+v" so the compiler takes them back from here and
+// never copies them before it).
+__device__ __forceinline__ void crypt_last_half_next_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls,
+                                                         u32x16 &addr, const u32x8 &lim, u32x2 sink, uint32_t &palo,
+                                                         uint32_t &pahi, uint32_t sb, uint32_t &nlen, uint64_t &noff,
+                                                         uint32_t nvalid, const uint8_t *payload)
+{
+    u32x16 X;
+    u32x8 T;
+    uint32_t b, k0, k1, a1s, s1, h, nb;
+    uint64_t full, msk;
+    asm volatile(
+        "s_mov_b64 %[full], exec\n\t"
+        ZRC4_NEXT_LINE0
+        ZRC4_LL_HALF_Q
+        "LL_DONE_%=:\n\t"
+        "s_mov_b64 exec, %[full]\n\t"
+        "s_waitcnt vmcnt(8)\n\t"             // the next line 0 (only this half's 8 stores are younger)
+        "s_nop 1\n\t"
+        : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1), [a0] "+v"(st.a0),
+          [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
+          [palo] "+v"(palo), [pahi] "+v"(pahi), [sb] "+s"(sb), [s1] "=&s"(s1),
+          [full] "=&s"(full), [msk] "=&s"(msk), [h] "=&v"(h), [nb] "=&v"(nb), [nlen] "+v"(nlen), [noff] "+v"(noff),
+          "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
+          "=&{v[144:151]}"(T)
+        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(ls.wmax), "{v[136:143]}"(lim),
+          "{v[152:153]}"(sink), [nv] "v"(nvalid), [pay] "s"(payload)
         : "memory", "vcc", "scc");
 }
 
-// One group's messages: head bytes, the line loop (lines 0 and 1 already in
-// P/Q), then 16-byte chunks and tail bytes.
-__device__ __forceinline__ void crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8_t *msg, uint32_t len,
-                                                  u32x32 &P, u32x32 &Q, const LineSetup &ls, uint8_t *sinkp)
+// One group's messages: head bytes, the line loop (line 0 in P, line 1 in
+// flight into Q), then 16-byte chunks and tail bytes.  With `want_next`, a
+// wave whose message has an even number of halves (>= 2) also fetches the
+// next group's line 0 into P before its final half (nlen / noff / nvalid:
+// that group's prefetched entry, crypt_last_half_next_asm); returns true when
+// it did.
+__device__ __forceinline__ bool crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8_t *msg, uint32_t len,
+                                                  u32x32 &P, u32x32 &Q, const LineSetup &ls, uint8_t *sinkp,
+                                                  bool want_next, uint32_t &nlen, uint64_t &noff, uint32_t nvalid,
+                                                  const uint8_t *payload)
 {
     const uint32_t head = head_bytes(msg, len);
     for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
     msg += head;
     len -= head;
+    bool got = false;
     if (ls.wmax) {
         u32x16 addr;
         u32x8 lim;
         line_roles(addr, lim, ls);
         const uint64_t s = (uint64_t)(uintptr_t)sinkp;
-        crypt_lines_asm(st, P, Q, ls, addr, lim, u32x2{(uint32_t)s, (uint32_t)(s >> 32)});
+        const u32x2 sk2 = u32x2{(uint32_t)s, (uint32_t)(s >> 32)};
+        const uint64_t pa = ls.p + 256u;                 // per-lane loads: blocks 4, 5 next
+        uint32_t palo = (uint32_t)pa, pahi = (uint32_t)(pa >> 32);
+        const uint32_t halves = (ls.wmax + 1u) >> 1;
+        got = want_next && halves >= 2u && !(halves & 1u);      // wave-uniform
+        const uint32_t sb = crypt_lines_asm(st, P, Q, ls, addr, lim, sk2, palo, pahi,
+                                            got ? 2u * (halves - 1u) : ls.wmax);
+        if (got)
+            crypt_last_half_next_asm(st, P, Q, ls, addr, lim, sk2, palo, pahi, sb, nlen, noff, nvalid, payload);
     }
     uint4 *p = reinterpret_cast<uint4 *>(msg + 64u * ls.nblk);
     uint32_t rem = len & 63u;
@@ -653,6 +745,7 @@ __device__ __forceinline__ void crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8
     }
     uint8_t *t = reinterpret_cast<uint8_t *>(p);
     for (uint32_t k = 0; k < rem; ++k) t[k] ^= (uint8_t)prga_step(S, st);
+    return got;
 }
 
 #define ZRC4_INVALID 0xFFFFFFFFu
@@ -1190,6 +1283,72 @@ __device__ __forceinline__ void prefetch_group(u32x32 &P, u32x32 &Q, u32x32 &ilo
         : "memory");
 }
 
+
+// crypt_stream_kernel's copy-out of a group's S-boxes at a group boundary:
+// all 16 LDS reads in flight at once, then the 16 stores (the compiler's
+// version paired them, one LDS round trip per pair, while the other
+// workgroup on the CU keeps the LDS busy).  v72..v135 (line 1, the transpose
+// spares and the store addresses of the line loop) are dead here.
+__device__ __forceinline__ void lds_to_image_asm(uint8_t *img, uint32_t tid)
+{
+    u32x32 d0, d1;
+    uint32_t vo;
+    asm volatile(
+        "v_lshlrev_b32 %[vo], 4, %[t]\n\t"
+        "ds_read_b128 v[72:75], %[vo]\n\t"
+        "ds_read_b128 v[76:79], %[vo] offset:4096\n\t"
+        "ds_read_b128 v[80:83], %[vo] offset:8192\n\t"
+        "ds_read_b128 v[84:87], %[vo] offset:12288\n\t"
+        "ds_read_b128 v[88:91], %[vo] offset:16384\n\t"
+        "ds_read_b128 v[92:95], %[vo] offset:20480\n\t"
+        "ds_read_b128 v[96:99], %[vo] offset:24576\n\t"
+        "ds_read_b128 v[100:103], %[vo] offset:28672\n\t"
+        "ds_read_b128 v[104:107], %[vo] offset:32768\n\t"
+        "ds_read_b128 v[108:111], %[vo] offset:36864\n\t"
+        "ds_read_b128 v[112:115], %[vo] offset:40960\n\t"
+        "ds_read_b128 v[116:119], %[vo] offset:45056\n\t"
+        "ds_read_b128 v[120:123], %[vo] offset:49152\n\t"
+        "ds_read_b128 v[124:127], %[vo] offset:53248\n\t"
+        "ds_read_b128 v[128:131], %[vo] offset:57344\n\t"
+        "ds_read_b128 v[132:135], %[vo] offset:61440\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "global_store_dwordx4 %[vo], v[72:75], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[76:79], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[80:83], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[84:87], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[88:91], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[92:95], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[96:99], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[100:103], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[104:107], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[108:111], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[112:115], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[116:119], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[120:123], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[124:127], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[128:131], %[img]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_store_dwordx4 %[vo], v[132:135], %[img]\n\t"
+        "s_nop 1\n\t"                          // store-data VGPRs: VMEM store -> VALU write hazard
+        : "=&{v[72:103]}"(d0), "=&{v[104:135]}"(d1), [vo] "=&v"(vo)
+        : [t] "v"(tid), [img] "s"(img)
+        : "memory");
+}
+
 template <bool PF>
 __global__ void __launch_bounds__(256, 2)
 crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
@@ -1207,6 +1366,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     uint8_t *sk = sink + (size_t)j * kSinkSlot;
     stream_stamp(sink, 0);
     uint32_t k_t = 0;                         // groups done (ZRC4_TIMING stamps)
+    bool p_async = false;                     // P = next group's line 0, loaded by the line loop
 
     uint32_t w = blockIdx.x;
     EntryIn cur;
@@ -1288,6 +1448,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         // nothing the compiler tracks is pending at the loop.  Line 1 goes out
         // now, behind the fill, and is waited for inside the loop.
         asm volatile("" : "+{v[40:71]}"(P));
+        p_async = false;
         if (ls.wmax > 2u) issue_line1_asm(Q, ls, sk);
         if constexpr (PF) {
             if (more) {
@@ -1303,7 +1464,10 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         {
             Rc4Lane st;
             lane_init(st, S, col, cur.xy);
-            crypt_message_dpp(S, st, payload + cur.off, cur.len, P, Q, ls, sk);
+            // Before the message's final half (even half counts) the next
+            // group's line 0 goes into P (crypt_last_half_next_asm).
+            p_async = crypt_message_dpp(S, st, payload + cur.off, cur.len, P, Q, ls, sk, PF && more, rlen, roff,
+                                        en < n ? 1u : 0u, payload);
             if (active && cur.len) xy[cur.slot] = lane_xy(st);
         }
         stream_stamp(sink, 2u + 2u * k_t);
@@ -1312,7 +1476,10 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         EntryIn nxt = {0u, ZRC4_INVALID, 0u, 0u};
         if (more) {
             if constexpr (PF) {
-                asm volatile("s_waitcnt vmcnt(16)" : "+v"(rlen), "+v"(roff), "+v"(rxy) :: "memory");
+                // (already waited for when line 0 went out early: a wait here
+                // would also wait for it)
+                if (!p_async)
+                    asm volatile("s_waitcnt vmcnt(16)" : "+v"(rlen), "+v"(roff), "+v"(rxy) :: "memory");
                 const bool v = en < n;
                 nxt.len = v ? rlen : 0u;
                 nxt.off = v ? roff : 0u;
@@ -1323,13 +1490,13 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             }
             // the loop's last two halves issue no loads, so P/Q are free again
             line_setup(ls, payload + nxt.off, nxt.len);
-            preload_line0(P, ls, sk);
+            if (!p_async) preload_line0(P, ls, sk);
         }
 
         // ---- this group's state back to HBM
         if (whole) {
             __syncthreads();
-            lds_to_image(arena + (size_t)g * kGroupBytes, S);
+            lds_to_image_asm(arena + (size_t)g * kGroupBytes, j);
         } else if (active && cur.len) {
             scatter_column(arena, cur.slot, S, col);
         }
