@@ -69,6 +69,21 @@ def by_place(rt: np.ndarray, hwid: np.ndarray, wgs: int, K: int) -> dict:
     from collections import Counter
     cnt = Counter(cuk.tolist())
     out["wgs_per_cu"] = dict(Counter(cnt.values()))
+    pairs = {}
+    for i, k in enumerate(cuk.tolist()):
+        pairs.setdefault(k, []).append(i)
+    means, diffs, uneq = [], [], []
+    for k, ix in pairs.items():
+        if len(ix) == 2:
+            a, b = ix
+            means.append((chain[a] + chain[b]) / 2)
+            diffs.append(abs(chain[a] - chain[b]))
+            uneq.append((abs(chain[a] - chain[b]), int(simd[a]), int(simd[b]), round(float(chain[a]), 1),
+                         round(float(chain[b]), 1)))
+    if means:
+        out["cu_pairs"] = {"std_of_cu_means": round(float(np.std(means)), 2),
+                           "mean_abs_diff_in_pair": round(float(np.mean(diffs)), 2),
+                           "most_unequal": [list(u[1:]) for u in sorted(uneq)[-8:]]}
     order = np.argsort(chain)
     out["fastest"] = [[int(xcc[i]), int(se[i]), int(cu[i]), round(float(chain[i]), 2)] for i in order[:6]]
     out["slowest"] = [[int(xcc[i]), int(se[i]), int(cu[i]), round(float(chain[i]), 2)] for i in order[-6:]]

@@ -502,6 +502,17 @@ typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+// ZRC4_PRIO (crypt_stream_kernel): the two workgroups of a CU share its SIMDs
+// (one wave of each per SIMD) and the older wave wins the issue arbitration,
+// so one workgroup runs ahead (a CU's two workgroups differ by up to 7 us per
+// group, profiles/r02/stream_tl_pairs.log) and the other finishes alone at the
+// 4-wave rate.  1: alternate which of a SIMD's two waves (wave slot parity,
+// HW_ID) has the higher priority from one group to the next (cfg5 288.4 ->
+// 284.2 us; alternating every line-loop half: 286.3, profiles/r02/ab_prio.log).
+#ifndef ZRC4_PRIO
+#define ZRC4_PRIO 1
+#endif
+
 #if defined(ZRC4_LL_AB) && ZRC4_LL_AB
 #include "ab/zrc4_line_loop_ab.inc"   // timing-only A/B builds (tools/ab_bench.py --no-check)
 #else
@@ -596,6 +607,13 @@ __device__ __forceinline__ void issue_line1_asm(u32x32 &Q, const LineSetup &ls, 
         : "=&{v[72:103]}"(Q)
         : [a0] "v"(b0), [a1] "v"(b1)
         : "memory");
+}
+
+__device__ __forceinline__ uint32_t hw_id()
+{
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    return hw;
 }
 
 // The line loop, halves sb = 0, 2, ... until sb >= wend (wend = wmax: the
@@ -1460,6 +1478,15 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         }
 
         // ---- keystream over this group's messages
+#if ZRC4_PRIO == 1
+        {
+            const uint32_t hw = hw_id();                 // ZRC4_PRIO (above the line loop)
+            if (((hw ^ k_t) & 1u) != 0u)
+                __builtin_amdgcn_s_setprio(2);
+            else
+                __builtin_amdgcn_s_setprio(1);
+        }
+#endif
         stream_stamp(sink, 1u + 2u * k_t);
         {
             Rc4Lane st;
