@@ -119,7 +119,10 @@ int zrc4_crypt_grouped(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payload,
                        void *stream);
 
 /* Host-pointer variants: copy to the device (pinned staging), run, copy back,
- * block until done.  payload_bytes bounds the host payload buffer. */
+ * block until done.  payload_bytes bounds the host payload buffer.
+ * zrc4_crypt_host with several ids buckets them by group itself and runs the
+ * zrc4_crypt_grouped path (a slot may appear once per call: a repeated slot
+ * returns ZRC4_ERR_INVALID_ARG and crypts nothing). */
 int zrc4_ksa_host(zrc4_ctx *ctx, const uint32_t *ids, const uint8_t *keys,
                   size_t keys_bytes, const uint64_t *key_off,
                   const uint32_t *key_len, uint32_t n);

@@ -165,6 +165,41 @@ def test_batch_small_scattered_ids(ctx, batch_small):
     _check_batch(ctx, b, ids, pay)
 
 
+def test_crypt_host_scattered_ids_grouped(built, torch_cuda):
+    """zrc4_crypt_host with many arbitrary ids buckets them by group (the
+    grouped kernel; > 128 buckets: whole-group workgroups); entry order and
+    payload layout stay the caller's; two calls continue the keystream.  A
+    repeated slot is refused and crypts nothing."""
+    rng = np.random.default_rng(123)
+    cap = 65536
+    n = 3000
+    ids = rng.permutation(cap)[:n].astype(np.uint32)
+    keys = [rng.integers(0, 256, 1 + int(rng.integers(0, 20)), dtype=np.uint8).tobytes() for _ in range(n)]
+    ref = [pyoracle.Rc4(k) for k in keys]
+    L = rng.integers(0, 300, n).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(L[:-1] + 3)]).astype(np.uint64)
+    data = rng.integers(0, 256, int(off[-1] + L[-1]) + 8, dtype=np.uint8)
+    with Context(0, cap) as c:
+        c.ksa_host(keys, ids=ids)
+        for call in range(2):
+            want = data.copy()
+            for i in range(n):
+                a, z = int(off[i]), int(off[i] + L[i])
+                want[a:z] = np.frombuffer(ref[i].encryption(want[a:z].tobytes()), np.uint8)
+            got = data.copy()
+            c.crypt_host(got, off, L, ids=ids)
+            assert np.array_equal(got, want), call
+            data = got
+        dup = ids[:10].copy()
+        dup[5] = dup[2]
+        before = c.get_state(int(dup[2]))
+        buf = np.zeros(10 * 16, dtype=np.uint8)
+        with pytest.raises(ZRC4Error) as ei:
+            c.crypt_host(buf, np.arange(10, dtype=np.uint64) * 16, np.full(10, 16, dtype=np.uint32), ids=dup)
+        assert ei.value.code == -1                 # ZRC4_ERR_INVALID_ARG
+        assert c.get_state(int(dup[2])) == before and not buf.any()
+
+
 def test_batch_whole_group_ids(ctx, batch_small):
     """ids given but exactly an aligned 256-slot group -> coalesced fast path."""
     rng = np.random.default_rng(9)

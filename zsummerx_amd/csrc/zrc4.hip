@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <vector>
 #include <new>
 
 #ifndef ZRC4_HALF
@@ -428,14 +429,54 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
             return ZRC4_ERR_INVALID_ARG;
     int rc = set_device(c);
     if (rc) return rc;
-    const size_t o_ids = 0, s_ids = ids ? align16((size_t)n * 4) : 0;
-    const size_t o_off = o_ids + s_ids, s_off = align16((size_t)n * 8);
-    const size_t o_len = o_off + s_off, s_len = align16((size_t)n * 4);
+    // Several arbitrary ids: bucket them by 256-slot group here (the
+    // zrc4_crypt_grouped contract), so every group's S-boxes move as one
+    // coalesced image instead of 256 strided byte accesses per slot.  A slot
+    // may appear once per call (as for every batched entry point).
+    const bool grouped = ids && n > 1;
+    std::vector<uint32_t> order;
+    uint32_t buckets = 0;
+    if (grouped) {
+        order.resize(n);
+        for (uint32_t i = 0; i < n; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ids[a] < ids[b]; });
+        for (uint32_t k = 0; k < n; ++k) {
+            if (k && ids[order[k]] == ids[order[k - 1]]) return ZRC4_ERR_INVALID_ARG;
+            if (!k || (ids[order[k]] >> 8) != (ids[order[k - 1]] >> 8)) ++buckets;
+        }
+    }
+    const uint32_t m = grouped ? buckets * zrc4::kGroup : n;      // entries the kernel sees
+    const size_t o_ids = 0, s_ids = ids ? align16((size_t)m * 4) : 0;
+    const size_t o_off = o_ids + s_ids, s_off = align16((size_t)m * 8);
+    const size_t o_len = o_off + s_off, s_len = align16((size_t)m * 4);
     const size_t o_pay = o_len + s_len, total = o_pay + align16(payload_bytes ? payload_bytes : 1);
     if ((rc = grow_stage(c, total))) return rc;
-    if (ids) memcpy(c->h_stage + o_ids, ids, (size_t)n * 4);
-    memcpy(c->h_stage + o_off, off, (size_t)n * 8);
-    memcpy(c->h_stage + o_len, len, (size_t)n * 4);
+    if (grouped) {
+        uint32_t *bi = reinterpret_cast<uint32_t *>(c->h_stage + o_ids);
+        uint64_t *bo = reinterpret_cast<uint64_t *>(c->h_stage + o_off);
+        uint32_t *bl = reinterpret_cast<uint32_t *>(c->h_stage + o_len);
+        for (uint32_t e = 0; e < m; ++e) {
+            bi[e] = ZRC4_IDLE_SLOT;
+            bo[e] = 0;
+            bl[e] = 0;
+        }
+        uint32_t b = 0, pos = 0;
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t i = order[k];
+            if (k && (ids[i] >> 8) != (ids[order[k - 1]] >> 8)) {
+                ++b;
+                pos = 0;
+            }
+            const uint32_t e = b * zrc4::kGroup + pos++;
+            bi[e] = ids[i];
+            bo[e] = off[i];
+            bl[e] = len[i];
+        }
+    } else {
+        if (ids) memcpy(c->h_stage + o_ids, ids, (size_t)n * 4);
+        memcpy(c->h_stage + o_off, off, (size_t)n * 8);
+        memcpy(c->h_stage + o_len, len, (size_t)n * 4);
+    }
     if (payload_bytes) memcpy(c->h_stage + o_pay, payload, payload_bytes);
     // Small batches (the per-call RC4Encryption::encryption drop-in) run on
     // the pinned staging copy in place: no H2D / D2H copies on the latency
@@ -446,8 +487,9 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
         ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
         st = c->d_stage;
     }
-    rc = launch_crypt(c, ids ? zrc4::kIds : zrc4::kRange, ids ? (const uint32_t *)(st + o_ids) : nullptr, 0,
-                      st + o_pay, (const uint64_t *)(st + o_off), (const uint32_t *)(st + o_len), n, c->stream);
+    rc = launch_crypt(c, grouped ? zrc4::kGrouped : ids ? zrc4::kIds : zrc4::kRange,
+                      ids ? (const uint32_t *)(st + o_ids) : nullptr, 0, st + o_pay, (const uint64_t *)(st + o_off),
+                      (const uint32_t *)(st + o_len), m, c->stream);
     if (rc) return rc;
     if (payload_bytes && !zero_copy)
         ZRC4_TRY(hipMemcpyAsync(c->h_stage + o_pay, c->d_stage + o_pay, payload_bytes,
