@@ -906,6 +906,9 @@ __device__ __forceinline__ void frame_walk(const uint8_t *b, uint32_t L, uint32_
 #ifndef ZRC4_HALF_PAD
 #define ZRC4_HALF_PAD 1
 #endif
+#ifndef ZRC4_WPERM
+#define ZRC4_WPERM 97
+#endif
 constexpr uint32_t kTabOff = kGroupBytes + 16;
 constexpr uint32_t kSidOff = kTabOff + 256 * 16;              // 16 B: the half-group workgroup's SIMD ids
 constexpr uint32_t kSmemDirect = kSidOff + 16;                // 69 664 B: two workgroups per CU
@@ -956,7 +959,19 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         if (w != a && w != b) return;                    // uniform (SGPR) branch: the wave ends
         tid = (w == a ? 0u : 64u) + (threadIdx.x & 63u);
     }
-    const uint32_t e = blockIdx.x * kLanes + tid;        // batch entry of this thread
+    // Which group (bucket) this workgroup runs: blockIdx.x, or (ZRC4_WPERM,
+    // whole groups) blockIdx.x * ZRC4_WPERM mod grid -- a bijection when the
+    // prime ZRC4_WPERM does not divide the grid -- so that the XCD a
+    // workgroup lands on (blockIdx.x mod 8) no longer follows the group
+    // order: cfg3 23.29 -> 22.72 us (profiles/r02/ab_wperm.log; a grouped
+    // batch, whose buckets come in random group order, moved 1.01x its
+    // algorithmic bytes against 1.10x for the same range batch).
+    uint32_t wg = blockIdx.x;
+    if constexpr (!HALF && ZRC4_WPERM != 0) {
+        constexpr uint32_t kMul = ZRC4_WPERM + 0u;
+        if (gridDim.x % kMul != 0u) wg = (blockIdx.x * kMul) % gridDim.x;
+    }
+    const uint32_t e = wg * kLanes + tid;                // batch entry of this thread
     const bool valid = e < n;
     const uint32_t h = HALF ? (blockIdx.x & 1u) : 0u;    // half of the group (HALF)
     const uint32_t j = h * 128u + tid;                   // group lane
@@ -974,7 +989,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         // Issued from asm, first: hipcc otherwise sinks these loads below its
         // wait for len/off.  Group (first_slot >> 8) + w lies inside the arena
         // even when first_slot is unaligned and the image goes unused.
-        g = (first_slot >> 8) + (HALF ? blockIdx.x >> 1 : blockIdx.x);
+        g = (first_slot >> 8) + (HALF ? blockIdx.x >> 1 : wg);
         issue_image_asm(ilo, ihi, arena + (size_t)g * kGroupBytes, vo0);
         whole = (first_slot & 255u) == 0u;
         ent = e;
@@ -989,7 +1004,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         //    across waves by one atomic min/max per wave) and the slot ->
         //    entry table; 3. lane j takes the entry of slot g*256 + j.
         constexpr uint32_t kPer = kGroup / kLanes;
-        const uint32_t w = HALF ? blockIdx.x >> 1 : blockIdx.x;
+        const uint32_t w = HALF ? blockIdx.x >> 1 : wg;
         uint32_t *te = reinterpret_cast<uint32_t *>(smem + kTabOff);          // entry index
         uint32_t *tl = te + 256;                                              // length
         uint64_t *to = reinterpret_cast<uint64_t *>(smem + kTabOff + 2048);   // offset
@@ -1089,7 +1104,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         mylen = slot != ZRC4_INVALID ? len[e] : 0u;
         myoff = slot != ZRC4_INVALID ? off[e] : 0u;
         sxy = mylen ? xy[slot] : (uint16_t)0;
-        const uint32_t first = ids[blockIdx.x * kGroup];
+        const uint32_t first = ids[wg * kGroup];
         g = first >> 8;
         if (tid == 0) flag[0] = 1u;
         __syncthreads();
