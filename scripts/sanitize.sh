@@ -17,3 +17,7 @@ export ZSX_STRESS="$ZSX_TOOLS_BIN/frame_stress_emu"
 export ASAN_OPTIONS="abort_on_error=1:detect_leaks=1:halt_on_error=1"
 export UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1"
 python -m pytest tests/test_hooks.py tests/test_frame.py -m "not gpu" -q -p no:cacheprovider "$@"
+# ThreadSanitizer over the reservoir's XOR worker threads (XorPool)
+python -c "from zsummerx_amd import build; build.build_test_tools(sanitize='thread')"
+ZSX_TOOLS_BIN="$PWD/tools/bin/tsan" TSAN_OPTIONS="halt_on_error=1" \
+    python -m pytest tests/test_hooks.py -m "not gpu" -q -p no:cacheprovider -k parallel "$@"

@@ -49,6 +49,16 @@ def test_reservoir_small_rings_emulated(tools, ring):
     assert out["hooks"]["tail_bytes"] > 0 and out["hooks"]["ring_bytes"] > 0
 
 
+@pytest.mark.parametrize("threads", [2, 4])
+def test_reservoir_parallel_xor_emulated(tools, threads):
+    """The host XOR spread over worker threads (XorPool) for every batch
+    (threshold 0): same bytes as the oracle, ring wrap included."""
+    import os
+    env = dict(os.environ, ZSX_XOR_THREADS=str(threads), ZSX_XOR_MIN_BYTES="0")
+    out = run(tools / "hooks_check_emu", "device", 64, 120, 13, 4096, env=env)
+    assert out["hooks"]["xor_threads"] == threads and out["hooks"]["ring_bytes"] > 0
+
+
 def test_direct_host_logic_emulated(tools):
     run(tools / "hooks_check_emu", "direct", 16, 40, 9)
 
@@ -59,6 +69,14 @@ def test_direct_host_logic_emulated(tools):
                                                         ("direct", 1024, 30, 4)])
 def test_device_hooks_vs_oracle(tools, mode, sessions, rounds, seed):
     run(tools / "hooks_check", mode, sessions, rounds, seed)
+
+
+@pytest.mark.gpu
+def test_device_hooks_parallel_xor(tools):
+    import os
+    env = dict(os.environ, ZSX_XOR_THREADS="4", ZSX_XOR_MIN_BYTES="0")
+    out = run(tools / "hooks_check", "device", 512, 60, 17, env=env)
+    assert out["hooks"]["xor_threads"] == 4 and out["hooks"]["ring_bytes"] > 0
 
 
 @pytest.mark.gpu

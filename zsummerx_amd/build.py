@@ -128,9 +128,10 @@ def build_frame(force: bool = False) -> Path:
 
 
 SANITIZE = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", "-g"]
+TSAN = ["-fsanitize=thread", "-g"]
 
 
-def build_test_tools(force: bool = False, sanitize: bool = False) -> Path:
+def build_test_tools(force: bool = False, sanitize: bool | str = False) -> Path:
     """Test infrastructure (links the oracle; never part of the product):
       tools/bin/hooks_check      the device Rc4Hooks driven like the engine,
                                  every byte checked against the oracle (GPU)
@@ -138,9 +139,12 @@ def build_test_tools(force: bool = False, sanitize: bool = False) -> Path:
                                  the zrc4 C-ABI (tests/cpp/emu_zrc4_hip.cpp)
       tools/bin/frame_stress_emu the engine + device hooks over that emulation
     sanitize=True builds only the two emulated binaries, with ASan + UBSan,
-    into tools/bin/san/ (scripts/sanitize.sh runs the CPU suites on them)."""
+    into tools/bin/san/ (scripts/sanitize.sh runs the CPU suites on them);
+    sanitize="thread" the same with ThreadSanitizer into tools/bin/tsan/ (the
+    reservoir's XOR worker threads)."""
     frame = build_frame(force)
-    out = ROOT / "tools" / "bin" / ("san" if sanitize else "")
+    sub = {False: "", True: "san", "thread": "tsan"}[sanitize]
+    out = ROOT / "tools" / "bin" / sub
     out.mkdir(parents=True, exist_ok=True)
     orc = ROOT / "oracle" / "liboracle.so"
     chk = ROOT / "tests" / "cpp" / "hooks_check.cpp"
@@ -162,7 +166,8 @@ def build_test_tools(force: bool = False, sanitize: bool = False) -> Path:
           *map(str, FRAME_SOURCES), str(emu), *oracle_link, "-ldl", "-lpthread"]),
     ]
     if sanitize:
-        jobs = [(t, d, [c[0], *SANITIZE, *c[1:], "-Wl,-rpath,$ORIGIN/../../../oracle"])
+        flags = TSAN if sanitize == "thread" else SANITIZE
+        jobs = [(t, d, [c[0], *flags, *c[1:], "-Wl,-rpath,$ORIGIN/../../../oracle"])
                 for t, d, c in jobs if t.name.endswith("_emu")]
     for target, deps, cmd in jobs:
         if force or _stale(target, deps):

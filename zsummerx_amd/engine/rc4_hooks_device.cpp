@@ -42,12 +42,16 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "zrc4.h"
@@ -204,6 +208,105 @@ void xorAndClear(uint8_t *__restrict dst, uint8_t *__restrict src, size_t n)
     std::memset(src, 0, n);
 }
 
+// One piece of a reservoir call's host work: span bytes ^= committed ring
+// bytes, ring bytes = 0.
+struct XorJob {
+    uint8_t *dst;
+    uint8_t *src;
+    uint32_t n;
+};
+
+// The reservoir's host XOR for large batches, spread over worker threads.
+// At 2 048 sessions x 2 in flight one call XORs 4 MiB (4 096 spans) and the
+// event loop spends ~1 ms in it on one core (profiles/r02/frame_loopback_v2.jsonl:
+// 975 us per call, slower than the direct GPU path).  Only the keystream XOR
+// is parallel: keystream generation stays on the GPU, and every piece of
+// bookkeeping stays on the calling thread.  Threads: $ZSX_XOR_THREADS
+// (default min(4, hardware threads / 2); 0 or 1 = inline); batches under
+// $ZSX_XOR_MIN_BYTES (default kParallelBytes) run inline.
+class XorPool {
+public:
+    static constexpr size_t kParallelBytes = 256u << 10;
+
+    XorPool()
+    {
+        if (const char *m = std::getenv("ZSX_XOR_MIN_BYTES")) minBytes_ = (size_t)std::strtoull(m, nullptr, 10);
+        const char *e = std::getenv("ZSX_XOR_THREADS");
+        unsigned hw = std::thread::hardware_concurrency();
+        unsigned t = e ? (unsigned)std::atoi(e) : std::min(4u, hw / 2u);
+        workers_ = t > 1u ? t - 1u : 0u;          // the calling thread is one of them
+        for (unsigned i = 0; i < workers_; ++i) threads_.emplace_back([this, i] { loop(i + 1u); });
+    }
+    ~XorPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (std::thread &t : threads_) t.join();
+    }
+    unsigned threads() const { return workers_ + 1u; }
+
+    void run(const std::vector<XorJob> &jobs, size_t bytes)
+    {
+        if (!workers_ || bytes < minBytes_ || jobs.size() < 2) {
+            for (const XorJob &j : jobs) xorAndClear(j.dst, j.src, j.n);
+            return;
+        }
+        // contiguous job ranges of about equal bytes, one per thread
+        const unsigned parts = workers_ + 1u;
+        bounds_.assign(parts + 1u, jobs.size());
+        bounds_[0] = 0;
+        size_t acc = 0, k = 1;
+        for (size_t i = 0; i < jobs.size() && k < parts; ++i) {
+            acc += jobs[i].n;
+            if (acc * parts >= bytes * k) bounds_[k++] = i + 1;
+        }
+        jobs_ = &jobs;
+        pending_.store(workers_, std::memory_order_relaxed);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            ++gen_;
+        }
+        cv_.notify_all();
+        work(0);
+        while (pending_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    }
+
+private:
+    void work(unsigned part)
+    {
+        const std::vector<XorJob> &jobs = *jobs_;
+        for (size_t i = bounds_[part]; i < bounds_[part + 1]; ++i) xorAndClear(jobs[i].dst, jobs[i].src, jobs[i].n);
+    }
+    void loop(unsigned part)
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> l(mu_);
+                cv_.wait(l, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+            }
+            work(part);
+            pending_.fetch_sub(1, std::memory_order_release);
+        }
+    }
+    unsigned workers_ = 0;
+    size_t minBytes_ = kParallelBytes;
+    std::vector<std::thread> threads_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+    const std::vector<XorJob> *jobs_ = nullptr;
+    std::vector<size_t> bounds_;
+    std::atomic<unsigned> pending_{0};
+};
+
 class DeviceRc4Hooks final : public Rc4Hooks {
 public:
     DeviceRc4Hooks(int device, uint32_t capacity, uint32_t ringBytes) : ringCap_(ringBytes)
@@ -331,9 +434,9 @@ public:
         std::snprintf(b, sizeof b,
                       "{\"ring_bytes\": %llu, \"tail_bytes\": %llu, \"tail_launches\": %llu, "
                       "\"refill_bytes\": %llu, \"refill_launches\": %llu, \"refill_waits\": %llu, "
-                      "\"ring_cap\": %u, \"refill_chunk\": %u, \"device_framed\": %llu}",
+                      "\"ring_cap\": %u, \"refill_chunk\": %u, \"device_framed\": %llu, \"xor_threads\": %u}",
                       ringBytes_, tailBytes_, tailLaunches_, refillBytes_, refillLaunches_, refillWaits_, ringCap_,
-                      refillChunk_, framed_);
+                      refillChunk_, framed_, xor_.threads());
         return b;
     }
 
@@ -396,8 +499,12 @@ private:
             ++refillWaits_;
             if ((rc = commitOldest(true)) != ZRC4_OK) return rc;
         }
-        // Host XOR with the committed ring bytes; collect the uncovered tails.
+        // Host XOR with the committed ring bytes (XorPool, after this pass:
+        // before any refill is launched, since a refill may write the ring
+        // bytes consumed here); collect the uncovered tails.
         es_.clear();
+        xj_.clear();
+        size_t xjBytes = 0;
         for (uint32_t i = 0; i < n; ++i) {
             const Rc4Span &sp = spans[i];
             if (!sp.len) continue;
@@ -409,11 +516,12 @@ private:
                 while (done < have) {
                     const uint32_t at = (uint32_t)((L.use + done) % ringCap_);
                     const uint32_t k = std::min(have - done, ringCap_ - at);
-                    xorAndClear(sp.data + done, r + at, k);
+                    xj_.push_back({sp.data + done, r + at, k});
                     done += k;
                 }
                 L.use += have;
                 ringBytes_ += have;
+                xjBytes += have;
             }
             if (have < sp.len) {
                 // the slot's device state is at position L.gen == L.use
@@ -427,6 +535,7 @@ private:
                 hungry_.push_back(sp.slot);
             }
         }
+        xor_.run(xj_, xjBytes);
         if (!es_.empty()) {
             if ((rc = drainRefills()) != ZRC4_OK) return rc;     // slot state must be quiet
             if ((rc = runTail(es_)) != ZRC4_OK) return rc;
@@ -612,6 +721,8 @@ private:
     uint32_t callStamp_ = 0;
     std::vector<uint8_t> hungryMark_;
     std::vector<uint32_t> hungry_;
+    std::vector<XorJob> xj_;
+    XorPool xor_;
     std::vector<Entry> es_, rs_;
     Table tt_;                                    // tail grouped table
     FrameTable ft_;                               // framing tables of cryptFrame
