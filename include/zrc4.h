@@ -198,6 +198,30 @@ int zrc4_crypt_grouped_frame(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payloa
                              const zrc4_frame_args *frame, void *stream);
 
 /* Wait for `stream`, then report (and clear) any latched device-side fault. */
+/* Keystream reservoir over a context (the C++ mirror's per-call path):
+ * per-slot rings of ring_bytes in pinned host memory that the device fills
+ * ahead with the slot's keystream (background stream, one grouped launch for
+ * every slot used since the last refill).  zrc4_ks_crypt XORs host spans with
+ * committed ring bytes on the host and crypts only what the rings do not
+ * cover on the device, so steady-state calls make no GPU round trip; output
+ * bytes are exactly RC4Encryption::encryption's.  Once a slot is used through
+ * a reservoir, every state change of it must go through the same reservoir
+ * (its device state runs ahead of its stream position by the buffered bytes):
+ * zrc4_ks_make_sbox == makeSBox, zrc4_ks_copy == copying the RC4Encryption
+ * value (device state + buffered keystream).  ring_bytes 0: no buffering
+ * (every call crypts on the device).  Thread-safe per reservoir; a slot at
+ * most once per zrc4_ks_crypt call.  stats: ring bytes, tail bytes, tail
+ * launches, refill bytes, refill launches, refill waits. */
+typedef struct zrc4_ks zrc4_ks;
+int zrc4_ks_create(zrc4_ctx *ctx, uint32_t ring_bytes, zrc4_ks **out);
+int zrc4_ks_destroy(zrc4_ks *ks);
+int zrc4_ks_crypt(zrc4_ks *ks, const uint32_t *ids, uint8_t *const *data,
+                  const uint32_t *len, uint32_t n);
+int zrc4_ks_make_sbox(zrc4_ks *ks, uint32_t id, const uint8_t *key,
+                      size_t keylen);
+int zrc4_ks_copy(zrc4_ks *dst_ks, uint32_t dst, zrc4_ks *src_ks, uint32_t src);
+int zrc4_ks_stats(zrc4_ks *ks, uint64_t out[6]);
+
 int zrc4_sync(zrc4_ctx *ctx, void *stream);
 
 /* Report (and clear) faults latched by kernels that have already completed

@@ -13,10 +13,14 @@
 //
 // Each RC4Encryption owns one slot (stream) of a process-wide device arena
 // that grows in 65 536-stream chunks.  A TcpSession owns two
-// (_rc4StateRead/_rc4StateWrite, session.h:115-116).  The per-call path runs
-// the kernel on a pinned staging copy of the caller's bytes (one launch and
-// one wait per call), so it is a correctness drop-in; the throughput path is
-// Rc4Batch or the batched engine (one launch per event-loop iteration).
+// (_rc4StateRead/_rc4StateWrite, session.h:115-116).  Every call goes through
+// the chunk's keystream reservoir (zrc4_ks_*, include/zrc4.h): the device
+// generates each slot's keystream ahead into a ring of pinned host memory
+// ($ZSX_RC4_RING bytes per slot, default 8192; 0 = no reservoir), so a call
+// is a host XOR with committed keystream and goes to the device only for
+// bytes the ring does not cover (a slot's first call after makeSBox, or a
+// burst larger than the ring).  Rc4Batch gathers one event-loop iteration's
+// calls into one reservoir call.
 #pragma once
 
 #include <cstdint>
@@ -54,6 +58,14 @@ public:
         std::lock_guard<std::mutex> g(mu_);
         return chunks_[slot / kChunk];
     }
+    // The chunk's keystream reservoir: every state change of a slot goes
+    // through it (zrc4.h: once used through a reservoir, a slot's device
+    // state runs ahead of its stream position).
+    zrc4_ks *ks(uint32_t slot)
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        return ks_[slot / kChunk];
+    }
     static uint32_t local(uint32_t slot) { return slot % kChunk; }
 
     uint32_t acquire()
@@ -67,7 +79,12 @@ public:
         if (next_ == (uint64_t)chunks_.size() * kChunk) {
             zrc4_ctx *c = nullptr;
             zrc4_throw(zrc4_create(&c, device_, kChunk), "zrc4_create");
+            zrc4_ks *k = nullptr;
+            const int rc = zrc4_ks_create(c, ring_, &k);
+            if (rc != ZRC4_OK) zrc4_destroy(c);
+            zrc4_throw(rc, "zrc4_ks_create");
             chunks_.push_back(c);
+            ks_.push_back(k);
         }
         return (uint32_t)next_++;
     }
@@ -76,15 +93,13 @@ public:
     // previous stream.
     void release(uint32_t s)
     {
-        zrc4_ctx *c = ctx(s);
-        uint8_t id[256];
-        for (int i = 0; i < 256; ++i) id[i] = (uint8_t)i;
-        const int rc = zrc4_set_state(c, local(s), id, 0, 0);
+        const int rc = zrc4_ks_make_sbox(ks(s), local(s), nullptr, 0);   // identity, ring emptied
         std::lock_guard<std::mutex> g(mu_);
         if (rc == ZRC4_OK) free_.push_back(s);   // a slot that cannot be reset is not reused
     }
     ~Rc4Arena()
     {
+        for (zrc4_ks *k : ks_) zrc4_ks_destroy(k);
         for (zrc4_ctx *c : chunks_) zrc4_destroy(c);
     }
 
@@ -93,10 +108,14 @@ private:
     {
         const char *d = std::getenv("ZSX_RC4_DEVICE");
         device_ = d ? std::atoi(d) : 0;
+        const char *r = std::getenv("ZSX_RC4_RING");
+        ring_ = r ? (uint32_t)std::strtoul(r, nullptr, 10) : 8192u;
     }
     int device_ = 0;
+    uint32_t ring_ = 8192;
     std::mutex mu_;
     std::vector<zrc4_ctx *> chunks_;
+    std::vector<zrc4_ks *> ks_;
     std::vector<uint32_t> free_;
     uint64_t next_ = 0;
 };
@@ -132,76 +151,67 @@ public:
     // identity box with x = y = 0.
     void makeSBox(std::string obscure)
     {
-        zrc4_throw(zrc4_make_sbox(Rc4Arena::instance().ctx(slot_), Rc4Arena::local(slot_),
-                                  reinterpret_cast<const uint8_t *>(obscure.data()),
-                                  obscure.size()),
+        zrc4_throw(zrc4_ks_make_sbox(Rc4Arena::instance().ks(slot_), Rc4Arena::local(slot_),
+                                     reinterpret_cast<const uint8_t *>(obscure.data()), obscure.size()),
                    "RC4Encryption::makeSBox");
     }
 
     // rc4_encryption.h:74-93 -- in place; length <= 0 does nothing.
     void encryption(unsigned char *data, int length)
     {
-        zrc4_throw(zrc4_encryption(Rc4Arena::instance().ctx(slot_), Rc4Arena::local(slot_), data, length),
-                   "RC4Encryption::encryption");
+        if (length <= 0) return;
+        const uint32_t id = Rc4Arena::local(slot_), n = (uint32_t)length;
+        uint8_t *d = data;
+        zrc4_throw(zrc4_ks_crypt(Rc4Arena::instance().ks(slot_), &id, &d, &n, 1), "RC4Encryption::encryption");
     }
 
     uint32_t slot() const { return slot_; }
 
 private:
     static constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+    // device state + the keystream already buffered for the source
     void copyState(const RC4Encryption &o)
     {
         Rc4Arena &a = Rc4Arena::instance();
-        uint8_t sb[256], x = 0, y = 0;
-        zrc4_throw(zrc4_get_state(a.ctx(o.slot_), Rc4Arena::local(o.slot_), sb, &x, &y), "RC4Encryption copy");
-        zrc4_throw(zrc4_set_state(a.ctx(slot_), Rc4Arena::local(slot_), sb, x, y), "RC4Encryption copy");
+        zrc4_throw(zrc4_ks_copy(a.ks(slot_), Rc4Arena::local(slot_), a.ks(o.slot_), Rc4Arena::local(o.slot_)),
+                   "RC4Encryption copy");
     }
     uint32_t slot_;
 };
 
 // Batched hook path: collect (slot, buffer, len) for one event-loop
-// iteration, then crypt them all with one launch.  Host buffers are gathered
-// into one pinned staging copy by zrc4_crypt_host.  Entries are crypted in
-// insertion order per slot; a slot may appear once per flush.  `slot` is a
-// slot of `ctx` (for RC4Encryption objects: Rc4Arena::local(r.slot()) of
-// the chunk Rc4Arena::instance().ctx(r.slot())).
+// iteration, then crypt them all with one reservoir call (host XOR for the
+// buffered keystream, one grouped launch for the uncovered tails).  A slot may
+// appear once per flush.  `slot` is a slot of the reservoir's chunk (for
+// RC4Encryption objects: Rc4Arena::local(r.slot()) with
+// Rc4Arena::instance().ks(r.slot())).
 class Rc4Batch {
 public:
-    explicit Rc4Batch(zrc4_ctx *ctx) : ctx_(ctx) {}
+    explicit Rc4Batch(zrc4_ks *ks) : ks_(ks) {}
     void add(uint32_t slot, unsigned char *data, unsigned len)
     {
         if (!len) return;
-        ptrs_.push_back(data);
         ids_.push_back(slot);
-        off_.push_back(bytes_.size());
+        ptrs_.push_back(data);
         len_.push_back(len);
-        bytes_.insert(bytes_.end(), data, data + len);
     }
     // Returns ZRC4_OK or the error; on error the caller closes the sessions
     // (the reference's BCT_CORRUPTION path, src/frame/session.cpp:355-361).
     int flush()
     {
         if (ids_.empty()) return ZRC4_OK;
-        int rc = zrc4_crypt_host(ctx_, ids_.data(), bytes_.data(), bytes_.size(), off_.data(),
-                                 len_.data(), (uint32_t)ids_.size());
-        if (rc == ZRC4_OK)
-            for (size_t i = 0; i < ids_.size(); ++i)
-                std::copy(bytes_.begin() + off_[i], bytes_.begin() + off_[i] + len_[i], ptrs_[i]);
-        ptrs_.clear();
+        const int rc = zrc4_ks_crypt(ks_, ids_.data(), ptrs_.data(), len_.data(), (uint32_t)ids_.size());
         ids_.clear();
-        off_.clear();
+        ptrs_.clear();
         len_.clear();
-        bytes_.clear();
         return rc;
     }
 
 private:
-    zrc4_ctx *ctx_;
-    std::vector<unsigned char *> ptrs_;
+    zrc4_ks *ks_;
     std::vector<uint32_t> ids_;
-    std::vector<uint64_t> off_;
+    std::vector<uint8_t *> ptrs_;
     std::vector<uint32_t> len_;
-    std::vector<uint8_t> bytes_;
 };
 
 }  // namespace zsummerx_amd

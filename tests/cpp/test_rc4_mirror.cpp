@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "zsummerx_amd/rc4_encryption.h"
+#include "rc4_oracle.h"   // test infrastructure: the CPU restatement (oracle/)
 
 using zsummerx_amd::RC4Encryption;
 using zsummerx_amd::Rc4Arena;
@@ -83,9 +84,9 @@ int main()
             for (size_t j = 0; j < plain[i].size(); ++j) plain[i][j] = (unsigned char)(i * 131 + j * 7);
             wire[i] = plain[i];
         }
-        zrc4_ctx *ctx = Rc4Arena::instance().ctx(cw[0].slot());
+        zrc4_ks *ks = Rc4Arena::instance().ks(cw[0].slot());
         for (int i = 0; i < kPeers; ++i) CHECK(cw[i].slot() / Rc4Arena::kChunk == 0 && sr[i].slot() / Rc4Arena::kChunk == 0);
-        Rc4Batch send_batch(ctx), recv_batch(ctx);
+        Rc4Batch send_batch(ks), recv_batch(ks);
         for (int i = 0; i < kPeers; ++i)
             send_batch.add(Rc4Arena::local(cw[i].slot()), wire[i].data(), (unsigned)wire[i].size());
         CHECK(send_batch.flush() == ZRC4_OK);
@@ -147,6 +148,60 @@ int main()
         std::memcpy(kp, "Plaintext", 9);
         for (int i = 0; i < 9; ++i) kp[i] ^= z[i];
         CHECK(hex(kp, 9) == "BBF316E8D940AF0AD3");
+    }
+    // The reservoir under a session's call pattern: many streams, calls of
+    // 0..3000 bytes (bursts larger than the ring), reseeds, copies taken
+    // mid-stream, batched and per-call paths mixed, every byte against the
+    // oracle; then the reservoir statistics show both host-XOR and device-tail
+    // bytes were exercised.
+    {
+        const int kStreams = 200, kRounds = 60;
+        std::vector<RC4Encryption> r(kStreams);
+        std::vector<oracle_rc4_state> o(kStreams);
+        uint64_t rng = 12345;
+        auto next = [&rng]() { rng = rng * 6364136223846793005ull + 1442695040888963407ull; return (uint32_t)(rng >> 33); };
+        for (int i = 0; i < kStreams; ++i) {
+            std::string key = "reservoir-" + std::to_string(i * 7919);
+            r[i].makeSBox(key);
+            oracle_make_sbox(&o[i], reinterpret_cast<const uint8_t *>(key.data()), key.size());
+        }
+        int bad = 0;
+        for (int round = 0; round < kRounds; ++round) {
+            zrc4_ks *ks = Rc4Arena::instance().ks(r[0].slot());
+            Rc4Batch batch(ks);
+            std::vector<std::vector<unsigned char>> bufs(kStreams), want(kStreams);
+            for (int i = 0; i < kStreams; ++i) {
+                const uint32_t n = (next() % 7 == 0) ? 1000 + next() % 2000 : next() % 600;
+                bufs[i].resize(n);
+                for (auto &b : bufs[i]) b = (unsigned char)next();
+                want[i] = bufs[i];
+                oracle_encryption(&o[i], want[i].data(), (long)n);
+                if (round % 2 == 0 && Rc4Arena::instance().ks(r[i].slot()) == ks)
+                    batch.add(Rc4Arena::local(r[i].slot()), bufs[i].data(), n);
+                else
+                    r[i].encryption(bufs[i].data(), (int)n);
+            }
+            CHECK(batch.flush() == ZRC4_OK);
+            for (int i = 0; i < kStreams; ++i) bad += bufs[i] != want[i];
+            if (round % 10 == 5) {              // reseed some, copy some
+                for (int i = 0; i < kStreams; i += 17) {
+                    std::string key = "re-" + std::to_string(round * 1000 + i);
+                    r[i].makeSBox(key);
+                    oracle_make_sbox(&o[i], reinterpret_cast<const uint8_t *>(key.data()), key.size());
+                }
+                for (int i = 3; i + 1 < kStreams; i += 29) {
+                    r[i + 1] = r[i];            // value copy mid-stream, keystream buffered or not
+                    o[i + 1] = o[i];
+                }
+            }
+        }
+        CHECK(bad == 0);
+        uint64_t st[6] = {0};
+        CHECK(zrc4_ks_stats(Rc4Arena::instance().ks(r[0].slot()), st) == ZRC4_OK);
+        std::printf("reservoir: ring %llu B, tail %llu B in %llu launches, refill %llu B in %llu launches, %llu waits\n",
+                    (unsigned long long)st[0], (unsigned long long)st[1], (unsigned long long)st[2],
+                    (unsigned long long)st[3], (unsigned long long)st[4], (unsigned long long)st[5]);
+        CHECK(st[0] > 0 && st[1] > 0 && st[4] > 0);
     }
     std::printf(fails ? "FAILED %d\n" : "ok\n", fails);
     return fails ? 1 : 0;

@@ -71,8 +71,10 @@ def test_no_device_is_a_loud_error(built):
 def _build_cpp_test(tmp_path):
     exe = tmp_path / "test_rc4_mirror"
     lib_dir = ROOT / "zsummerx_amd"
-    cmd = ["g++", "-O2", "-std=c++17", f"-I{ROOT / 'include'}", str(ROOT / "tests" / "cpp" / "test_rc4_mirror.cpp"),
-           f"-L{lib_dir}", "-lzrc4", f"-Wl,-rpath,{lib_dir}", "-o", str(exe)]
+    orc = ROOT / "oracle"
+    cmd = ["g++", "-O2", "-std=c++17", f"-I{ROOT / 'include'}", f"-I{orc}",
+           str(ROOT / "tests" / "cpp" / "test_rc4_mirror.cpp"), f"-L{lib_dir}", "-lzrc4", f"-Wl,-rpath,{lib_dir}",
+           f"-L{orc}", "-loracle", f"-Wl,-rpath,{orc}", "-o", str(exe)]
     subprocess.run(cmd, check=True)
     return exe
 

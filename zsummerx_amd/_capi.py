@@ -44,6 +44,12 @@ SIGNATURES = [
     ("zrc4_encryption", C.c_int, [_P, C.c_uint32, _P, C.c_int]),
     ("zrc4_xor_ring", C.c_int, [_P, _P, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_frame_scan", C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P]),
+    ("zrc4_ks_create", C.c_int, [_P, C.c_uint32, C.POINTER(_P)]),
+    ("zrc4_ks_destroy", C.c_int, [_P]),
+    ("zrc4_ks_crypt", C.c_int, [_P, _P, _P, _P, C.c_uint32]),
+    ("zrc4_ks_make_sbox", C.c_int, [_P, C.c_uint32, _P, C.c_size_t]),
+    ("zrc4_ks_copy", C.c_int, [_P, C.c_uint32, _P, C.c_uint32]),
+    ("zrc4_ks_stats", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("zrc4_sync", C.c_int, [_P, _P]),
     ("zrc4_poll_faults", C.c_int, [_P]),
     ("zrc4_get_state", C.c_int, [_P, C.c_uint32, _U8P, _U8P, _U8P]),

@@ -33,7 +33,8 @@ FRAME_DEPS = FRAME_SOURCES + [ROOT / "include" / "zsummerx_amd" / "frame.h",
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
 HIP_SOURCES = [CSRC / "zrc4.hip"]
-HIP_DEPS = HIP_SOURCES + [CSRC / "zrc4_kernels.hpp", CSRC / "zrc4_line_loop.inc", ROOT / "include" / "zrc4.h"]
+HIP_DEPS = HIP_SOURCES + [CSRC / "zrc4_kernels.hpp", CSRC / "zrc4_line_loop.inc", CSRC / "zrc4_ks.inc",
+                         ROOT / "include" / "zrc4.h"]
 
 
 def _hipcc() -> str:
@@ -77,6 +78,7 @@ def build_variant(name: str, defines: dict, rev: str | None = None) -> Path:
         for rel, dst in (("zsummerx_amd/csrc/zrc4.hip", tree / "csrc" / "zrc4.hip"),
                          ("zsummerx_amd/csrc/zrc4_kernels.hpp", tree / "csrc" / "zrc4_kernels.hpp"),
                          ("zsummerx_amd/csrc/zrc4_line_loop.inc", tree / "csrc" / "zrc4_line_loop.inc"),
+                         ("zsummerx_amd/csrc/zrc4_ks.inc", tree / "csrc" / "zrc4_ks.inc"),
                          ("include/zrc4.h", tree / "include" / "zrc4.h")):
             got = subprocess.run(["git", "show", f"{rev}:{rel}"], cwd=ROOT, capture_output=True)
             if got.returncode != 0:
@@ -175,6 +177,19 @@ def build_test_tools(force: bool = False, sanitize: bool | str = False) -> Path:
     return out
 
 
+def build_mirror_bench(force: bool = False) -> Path:
+    """tools/bin/mirror_bench: per-call cost of the drop-in RC4Encryption mirror
+    (tools/mirror_bench.cpp)."""
+    src = ROOT / "tools" / "mirror_bench.cpp"
+    out = ROOT / "tools" / "bin" / "mirror_bench"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    deps = [src, LIB, ROOT / "include" / "zsummerx_amd" / "rc4_encryption.h", ROOT / "include" / "zrc4.h"]
+    if force or _stale(out, deps):
+        subprocess.run(["g++", "-O2", "-std=c++17", f"-I{ROOT / 'include'}", str(src), f"-L{PKG}", "-lzrc4",
+                        "-Wl,-rpath,$ORIGIN/../../zsummerx_amd", "-o", str(out)], check=True)
+    return out
+
+
 def build_ubench(force: bool = False) -> None:
     """tools/ubench/traffic_calib: the known-byte-count kernels the PMC
     traffic passes calibrate FETCH_SIZE against (scripts/pmc_traffic.sh)."""
@@ -195,6 +210,7 @@ def build_all(force: bool = False) -> None:
     build_oracle()
     build_test_tools(force)
     build_ubench(force)
+    build_mirror_bench(force)
 
 
 if __name__ == "__main__":

@@ -589,3 +589,5 @@ int zrc4_debug_sink(zrc4_ctx *c, void **out)
 #endif
 
 }  // extern "C"
+
+#include "zrc4_ks.inc"   // keystream reservoirs (zrc4_ks_*)
