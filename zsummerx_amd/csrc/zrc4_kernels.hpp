@@ -254,13 +254,26 @@ __device__ __forceinline__ uint4 xor16(uint8_t *S, Rc4Lane &st, uint4 v)
 // XC = address of S[x] for this step; XN = address of S[x+1], derived from XC
 // inside the step right before its read.  XC is free after the S[x] = b write.
 // Per byte: 4 VALU + 5 LDS + 2 waits.
+// x + 1: ZRC4_XADD16 (default) adds 0x100 (SGPR operand c100) with a 16-bit
+// add, whose wrap at 65 536 is the mod-256 wrap of byte 1 (XN and XC hold
+// the same col in byte 0, bits 16-31 stay zero): a 4-byte VOP2 encoding
+// instead of the 8-byte SDWA add.
+#ifndef ZRC4_XADD16
+#define ZRC4_XADD16 1
+#endif
+#if ZRC4_XADD16
+#define ZRC4_XINC(XC, XN) "v_add_u16_e32 %[" #XN "], %[c100], %[" #XC "]\n\t"
+#else
+#define ZRC4_XINC(XC, XN)                                                                        \
+    "v_add_u32_sdwa %[" #XN "], 1, %[" #XC "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "        \
+    "src0_sel:DWORD src1_sel:BYTE_1\n\t"
+#endif
 #define ZRC4_CORE(XC, XN, A, P, K)                                                               \
     "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
     "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
     "ds_read_u8 %[b], %[ya]\n\t"                                                                 \
     "ds_write_b8 %[ya], %[" #A "]\n\t"                                                           \
-    "v_add_u32_sdwa %[" #XN "], 1, %[" #XC "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "        \
-    "src0_sel:DWORD src1_sel:BYTE_1\n\t"                                                         \
+    ZRC4_XINC(XC, XN)                                                                            \
     "ds_read_u8 %[" #P "], %[" #XN "]\n\t"                                                       \
     "s_waitcnt lgkmcnt(2)\n\t"                                                                   \
     "ds_write_b8 %[" #XC "], %[b]\n\t"                                                           \
@@ -414,7 +427,7 @@ __device__ __forceinline__ void crypt_blocks_asm(Rc4Lane &st, uint4 *&p, uint32_
           "+{v[40:43]}"(a0), "+{v[44:47]}"(a1), "+{v[48:51]}"(a2), "+{v[52:55]}"(a3),
           "=&{v[56:59]}"(b0), "=&{v[60:63]}"(b1), "=&{v[64:67]}"(b2), "=&{v[68:71]}"(b3),
           "=&{v[72:75]}"(q0), "=&{v[76:79]}"(q1), "=&{v[80:83]}"(q2), "=&{v[84:87]}"(q3)
-        : [nblk] "v"(nblk)
+        : [nblk] "v"(nblk), [c100] "s"(0x100u)
         : "memory", "vcc", "scc");
     p = reinterpret_cast<uint4 *>((uintptr_t)pa);
 }
@@ -644,7 +657,8 @@ __device__ __forceinline__ uint32_t crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x
           [full] "=&s"(full), [msk] "=&s"(msk),
           "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
           "=&{v[144:151]}"(T)
-        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(wend), "{v[136:143]}"(lim), "{v[152:153]}"(sink)
+        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(wend), "{v[136:143]}"(lim), "{v[152:153]}"(sink),
+          [c100] "s"(0x100u)
         : "memory", "vcc", "scc");
     return sb;
 }
@@ -719,7 +733,7 @@ __device__ __forceinline__ void crypt_last_half_next_asm(Rc4Lane &st, u32x32 &P,
           "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
           "=&{v[144:151]}"(T)
         : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(ls.wmax), "{v[136:143]}"(lim),
-          "{v[152:153]}"(sink), [nv] "v"(nvalid), [pay] "s"(payload)
+          "{v[152:153]}"(sink), [nv] "v"(nvalid), [pay] "s"(payload), [c100] "s"(0x100u)
         : "memory", "vcc", "scc");
 }
 
