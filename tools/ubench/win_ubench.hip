@@ -1,0 +1,335 @@
+// win_ubench.hip -- lane-parallel speculative RC4 windows (tools/window_sim.py)
+// as a keystream-only kernel: 8 lanes per stream, one window of up to 8 PRGA
+// steps per iteration.  Checks every keystream byte and final state against a
+// serial CPU PRGA and reports cycles per byte per stream.
+//   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/ubench/win_ubench.hip -o tools/ubench/win_ubench
+//   run:   tools/ubench/win_ubench [streams] [bytes] [W=8|16] [waves_per_block]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include <random>
+#include <algorithm>
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+constexpr int MAXN = 1024;       // keystream ring per stream (bytes)
+
+// Lean variant, W = 8 or 16 lanes per stream: one-hot cut bits from
+// med3(d, l, W), min-lane markers (ds_max of (tag << 8) | (255 - l)) for the
+// duplicate-j rule and for K's "written by a committed step <= l" test, y'
+// summed in-lane from the window bytes (no cross-lane gather).
+template <int W>
+__device__ __forceinline__ uint32_t orW(uint32_t v)
+{
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    if (W == 16) v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t mask_lt(uint32_t c, uint32_t q)   // bytes k < c of dword q
+{
+    return c <= 4 * q ? 0u : (c >= 4 * q + 4 ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (32 - 8 * (c - 4 * q))));
+}
+
+template <int W, int WPB>
+__global__ void __launch_bounds__(64 * WPB)
+win_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+           uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int SPW = 64 / W;                 // streams per wave
+    constexpr int ND = W / 4;                   // window dwords
+    __shared__ __attribute__((aligned(16))) uint8_t Sb[WPB * SPW * 256];
+    __shared__ uint32_t Mk[WPB * SPW * 256];
+    __shared__ __attribute__((aligned(16))) uint8_t Ring[WPB * SPW * MAXN];
+
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t l = lane % W, g = wv * SPW + lane / W;
+    const int s = blockIdx.x * (WPB * SPW) + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 256;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) S[l * (256 / W) + k] = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+    for (int k = 0; k < 256 / W; ++k) M[l * (256 / W) + k] = 0;
+    uint32_t xa = live ? ((xy_in[s] + 1) & 0xFF) : 1, y = live ? (xy_in[s] >> 8) : 0;
+    __syncthreads();
+
+    uint32_t m[ND];
+#pragma unroll
+    for (int q = 0; q < ND; ++q) m[q] = mask_lt(l + 1, q);
+    const uint32_t sel_l = 0x0C0C0C00u | (l & 3);
+    uint32_t V = (1u << 8) | (255 - l);         // marker value of this lane, tag in bits 8+
+    uint32_t rem = live ? (uint32_t)N : 0u, p = 0, nw = 0;
+    const uint32_t *S32 = reinterpret_cast<const uint32_t *>(S);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_ballot_w64(rem != 0)) {
+        nw += rem != 0;
+        uint32_t D[ND + 1], A[ND];
+        const uint32_t w0 = xa >> 2;
+#pragma unroll
+        for (int q = 0; q <= ND; ++q) D[q] = S32[(w0 + q) & 63];
+#pragma unroll
+        for (int q = 0; q < ND; ++q) A[q] = __builtin_amdgcn_alignbyte(D[q + 1], D[q], xa);
+        uint32_t J = y;
+#pragma unroll
+        for (int q = 0; q < ND; ++q) J = __builtin_amdgcn_sad_u8(A[q] & m[q], 0, J);
+        J &= 255;
+        uint32_t aw = A[0];
+#pragma unroll
+        for (int q = 1; q < ND; ++q) aw = (l >> 2) == (uint32_t)q ? A[q] : aw;
+        const uint32_t a = __builtin_amdgcn_perm(0, aw, sel_l);
+        const uint32_t b = S[J];
+        atomicMax(&M[J], V);
+        const uint32_t mr = __hip_atomic_load(&M[J], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t d = (J - xa) & 255;
+        const uint32_t c = d < l ? l : (d < (uint32_t)W ? d : (uint32_t)W);  // med3(d, l, W)
+        uint32_t oh = ((1u << c) | (mr != V ? (1u << l) : 0u)) & ~1u;
+        oh = orW<W>(oh | (1u << W));
+        uint32_t cut = __builtin_ctz(oh);
+        cut = cut < rem ? cut : rem;
+        const uint32_t t = (a + b) & 255;
+        const uint32_t k0 = S[t];
+        if (l < cut) {
+            S[(xa + l) & 255] = (uint8_t)b;
+            S[J] = (uint8_t)a;
+        }
+        const uint32_t k1 = S[t];
+        const uint32_t mt = M[t];
+        const bool own = ((t - xa) & 255) <= l || mt >= V;
+        if (l < cut) R[(p + l) & (MAXN - 1)] = (uint8_t)(own ? k1 : k0);
+#pragma unroll
+        for (int q = 0; q < ND; ++q) y = __builtin_amdgcn_sad_u8(A[q] & mask_lt(cut, q), 0, y);
+        y &= 255;
+        xa = (xa + cut) & 255;
+        p += cut;
+        rem -= cut;
+        V += 256;
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((xa - 1) & 255) | (y << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = nw;
+        }
+    }
+}
+
+
+// v3: S-box stored twice (S[p] and S[p + 256] written together, so a window
+// never wraps and reads as 5 aligned dwords), a_l read directly, y' from a
+// DPP max over lanes (l < cut ? l << 8 | J : 0) computed under the next
+// window's read round trip.
+template <int W>
+__device__ __forceinline__ uint32_t maxW(uint32_t v)
+{
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+    if (W == 16) v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+    return v;
+}
+
+template <int W, int WPB>
+__global__ void __launch_bounds__(64 * WPB)
+win3_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+            uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int SPW = 64 / W;
+    constexpr int ND = W / 4;
+    __shared__ __attribute__((aligned(16))) uint8_t Sb[WPB * SPW * 512];
+    __shared__ uint32_t Mk[WPB * SPW * 256];
+    __shared__ __attribute__((aligned(16))) uint8_t Ring[WPB * SPW * MAXN];
+
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t l = lane % W, g = wv * SPW + lane / W;
+    const int s = blockIdx.x * (WPB * SPW) + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 512;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        const uint8_t v = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        S[l * (256 / W) + k] = v;
+        S[256 + l * (256 / W) + k] = v;
+        M[l * (256 / W) + k] = 0;
+    }
+    uint32_t xa = live ? ((xy_in[s] + 1) & 0xFF) : 1, y = live ? (xy_in[s] >> 8) : 0;
+    __syncthreads();
+
+    uint32_t m[ND];
+#pragma unroll
+    for (int q = 0; q < ND; ++q) m[q] = mask_lt(l + 1, q);
+    uint32_t V = (1u << 8) | (255 - l);
+    uint32_t rem = live ? (uint32_t)N : 0u, p = 0, nw = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_ballot_w64(rem != 0)) {
+        nw += rem != 0;
+        const uint32_t *Wp = reinterpret_cast<const uint32_t *>(S + (xa & 0xFCu));
+        uint32_t D[ND + 1], A[ND];
+#pragma unroll
+        for (int q = 0; q <= ND; ++q) D[q] = Wp[q];
+        const uint32_t a = S[xa + l];
+#pragma unroll
+        for (int q = 0; q < ND; ++q) A[q] = __builtin_amdgcn_alignbyte(D[q + 1], D[q], xa);
+        uint32_t J = y;
+#pragma unroll
+        for (int q = 0; q < ND; ++q) J = __builtin_amdgcn_sad_u8(A[q] & m[q], 0, J);
+        J &= 255;
+        const uint32_t b = S[J];
+        atomicMax(&M[J], V);
+        const uint32_t mr = __hip_atomic_load(&M[J], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t d = (J - xa) & 255;
+        const uint32_t c = min(max(d, l), (uint32_t)W);   // med3(d, l, W)
+        uint32_t oh = ((1u << c) | (mr != V ? (1u << l) : 0u)) & ~1u;
+        oh = orW<W>(oh | (1u << W));
+        uint32_t cut = __builtin_ctz(oh);
+        cut = cut < rem ? cut : rem;
+        const uint32_t t = (a + b) & 255;
+        const uint32_t k0 = S[t];
+        if (l < cut) {
+            const uint32_t i = (xa + l) & 255;
+            S[i] = (uint8_t)b;
+            S[i + 256] = (uint8_t)b;
+            S[J] = (uint8_t)a;
+            S[J + 256] = (uint8_t)a;
+        }
+        const uint32_t k1 = S[t];
+        const uint32_t mt = M[t];
+        const bool own = ((t - xa) & 255) <= l || mt >= V;
+        if (l < cut) R[(p + l) & (MAXN - 1)] = (uint8_t)(own ? k1 : k0);
+        const uint32_t yl = maxW<W>(l < cut ? ((l + 1) << 8) | J : 0u);
+        y = cut ? (yl & 255) : y;
+        xa = (xa + cut) & 255;
+        p += cut;
+        rem -= cut;
+        V += 256;
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((xa - 1) & 255) | (y << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = nw;
+        }
+    }
+}
+
+static void ksa(uint8_t *S, const uint8_t *key, int kl)
+{
+    for (int i = 0; i < 256; ++i) S[i] = (uint8_t)i;
+    int j = 0;
+    for (int i = 0; i < 256; ++i) {
+        j = (j + S[i] + (kl ? key[i % kl] : 0)) & 255;
+        std::swap(S[i], S[j]);
+    }
+}
+
+static void prga(uint8_t *S, uint32_t &x, uint32_t &y, uint8_t *out, int n)
+{
+    for (int k = 0; k < n; ++k) {
+        x = (x + 1) & 255;
+        const uint8_t a = S[x];
+        y = (y + a) & 255;
+        const uint8_t b = S[y];
+        S[x] = b;
+        S[y] = a;
+        out[k] = S[(a + b) & 255];
+    }
+}
+
+template <int W, int WPB, int V3>
+static void run(int ns, int N, int reps)
+{
+    std::mt19937 rng(7);
+    std::vector<uint8_t> sb((size_t)ns * 256), sbw((size_t)ns * 256), ksw((size_t)ns * N), tmp(4096);
+    std::vector<uint16_t> xy(ns), xyw(ns);
+    for (int s = 0; s < ns; ++s) {
+        uint8_t key[40];
+        const int kl = rng() % 40;
+        for (int k = 0; k < kl; ++k) key[k] = (uint8_t)rng();
+        ksa(&sb[(size_t)s * 256], key, kl);
+        uint32_t x = 0, y = 0;
+        prga(&sb[(size_t)s * 256], x, y, tmp.data(), rng() % 600);   // mid-stream state
+        xy[s] = (uint16_t)(x | (y << 8));
+        memcpy(&sbw[(size_t)s * 256], &sb[(size_t)s * 256], 256);
+        prga(&sbw[(size_t)s * 256], x, y, &ksw[(size_t)s * N], N);
+        xyw[s] = (uint16_t)(x | (y << 8));
+    }
+    uint8_t *dsb, *dks, *dsbo;
+    uint16_t *dxy, *dxyo;
+    uint64_t *dcyc;
+    uint32_t *dwin;
+    CHECK(hipMalloc(&dsb, sb.size()));
+    CHECK(hipMalloc(&dsbo, sb.size()));
+    CHECK(hipMalloc(&dks, ksw.size()));
+    CHECK(hipMalloc(&dxy, ns * 2));
+    CHECK(hipMalloc(&dxyo, ns * 2));
+    CHECK(hipMalloc(&dcyc, ns * 8));
+    CHECK(hipMalloc(&dwin, ns * 4));
+    CHECK(hipMemcpy(dsb, sb.data(), sb.size(), hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dxy, xy.data(), ns * 2, hipMemcpyHostToDevice));
+    const int blocks = (ns + WPB * (64 / W) - 1) / (WPB * (64 / W));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    std::vector<float> ms;
+    for (int r = 0; r < reps; ++r) {
+        CHECK(hipEventRecord(e0));
+        if (V3) win3_kernel<W, WPB><<<blocks, 64 * WPB>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else win_kernel<W, WPB><<<blocks, 64 * WPB>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float t;
+        CHECK(hipEventElapsedTime(&t, e0, e1));
+        ms.push_back(t);
+    }
+    std::vector<uint8_t> ks(ksw.size()), sbo(sb.size());
+    std::vector<uint16_t> xyo(ns);
+    std::vector<uint64_t> cyc(ns);
+    std::vector<uint32_t> win(ns);
+    CHECK(hipMemcpy(ks.data(), dks, ks.size(), hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(sbo.data(), dsbo, sbo.size(), hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(xyo.data(), dxyo, ns * 2, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(cyc.data(), dcyc, ns * 8, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(win.data(), dwin, ns * 4, hipMemcpyDeviceToHost));
+    long bad_ks = 0, bad_st = 0, first = -1;
+    for (size_t i = 0; i < ks.size(); ++i)
+        if (ks[i] != ksw[i]) { ++bad_ks; if (first < 0) first = (long)i; }
+    for (int s = 0; s < ns; ++s)
+        if (memcmp(&sbo[(size_t)s * 256], &sbw[(size_t)s * 256], 256) || xyo[s] != xyw[s]) ++bad_st;
+    double cs = 0, ws = 0;
+    uint64_t cmax = 0;
+    for (int s = 0; s < ns; ++s) { cs += (double)cyc[s]; ws += win[s]; if (cyc[s] > cmax) cmax = cyc[s]; }
+    std::sort(ms.begin(), ms.end());
+    printf("{\"v3\": %d, \"W\": %d, \"wpb\": %d, \"streams\": %d, \"bytes\": %d, \"bad_ks\": %ld, \"first_bad\": %ld, \"bad_state\": %ld, "
+           "\"memtime_per_byte_mean\": %.2f, \"memtime_per_byte_max\": %.2f, \"bytes_per_window\": %.3f, "
+           "\"kernel_ms_median\": %.4f, \"ns_per_byte\": %.2f}\n",
+           V3, W, WPB, ns, N, bad_ks, first, bad_st, cs / ns / N, (double)cmax / N, (double)ns * N / ws,
+           ms[ms.size() / 2], ms[ms.size() / 2] * 1e6 / N);
+    (void)hipFree(dsb); (void)hipFree(dsbo); (void)hipFree(dks); (void)hipFree(dxy); (void)hipFree(dxyo); (void)hipFree(dcyc); (void)hipFree(dwin);
+}
+
+int main(int argc, char **argv)
+{
+    const int ns = argc > 1 ? atoi(argv[1]) : 4096;
+    const int N = argc > 2 ? atoi(argv[2]) : 1024;
+    const int w = argc > 3 ? atoi(argv[3]) : 16;
+    const int wpb = argc > 4 ? atoi(argv[4]) : 1;
+    if (N > MAXN || N % 16) { printf("bytes must be a multiple of 16 and <= %d\n", MAXN); return 1; }
+    const int v3 = argc > 5 ? atoi(argv[5]) : 1;
+    if (v3) { if (w == 8) run<8, 1, 1>(ns, N, 20); else if (wpb == 1) run<16, 1, 1>(ns, N, 20); else run<16, 2, 1>(ns, N, 20); }
+    else if (w == 8) { if (wpb == 1) run<8, 1, 0>(ns, N, 20); else run<8, 2, 0>(ns, N, 20); }
+    else { if (wpb == 1) run<16, 1, 0>(ns, N, 20); else run<16, 2, 0>(ns, N, 20); }
+    return 0;
+}
