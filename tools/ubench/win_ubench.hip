@@ -225,6 +225,172 @@ win3_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint
     }
 }
 
+
+// v4: the W = 16 window loop as one asm statement (hand-scheduled):
+//   reads of window n issue first; the tail of window n-1 (y' max over lanes,
+//   keystream select, ring write) runs under their round trip; the prefix
+//   (alignbyte, and, sad tree) -> b / marker reads -> rules under that round
+//   trip -> marker rule -> DPP OR -> cut -> k0 read -> commit (4 writes, both
+//   S copies) -> k1 / marker(t) reads -> state updates.
+// Pinned temporaries: v100-v104 window dwords, v105-v135 scratch; s[40:47].
+#define WIN_TAIL                                                                                  \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v120, v120, v120 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"           \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v120, v120, v120 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"           \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v120, v120, v120 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"               \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v120, v120, v120 row_mirror row_mask:0xf bank_mask:0xf\n\t"                    \
+    "s_waitcnt lgkmcnt(%[tailcnt])\n\t"                                                           \
+    "v_cmp_ge_u32_e64 s[42:43], v123, %[v]\n\t"                                                   \
+    "s_or_b64 s[42:43], s[42:43], s[44:45]\n\t"                                                   \
+    "v_cndmask_b32_e64 v124, v121, v122, s[42:43]\n\t"                                            \
+    "s_mov_b64 s[40:41], exec\n\t"                                                                \
+    "s_mov_b64 exec, s[46:47]\n\t"                                                                \
+    "ds_write_b8 v125, v124\n\t"                                                                  \
+    "s_mov_b64 exec, s[40:41]\n\t"                                                                \
+    "v_and_b32 %[y], 0xff, v120\n\t"                                                              \
+    "v_add_u32 %[v], 0x100, %[v]\n\t"
+
+template <int WPB>
+__global__ void __launch_bounds__(64 * WPB)
+win4_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+            uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int W = 16, SPW = 4;
+    __shared__ __attribute__((aligned(1024))) uint32_t Mk[WPB * SPW * 256];
+    __shared__ __attribute__((aligned(1024))) uint8_t Ring[WPB * SPW * MAXN];
+    __shared__ __attribute__((aligned(512))) uint8_t Sb[WPB * SPW * 512];
+
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t l = lane % W, g = wv * SPW + lane / W;
+    const int s = blockIdx.x * (WPB * SPW) + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 512;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        const uint8_t v = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        S[l * (256 / W) + k] = v;
+        S[256 + l * (256 / W) + k] = v;
+        M[l * (256 / W) + k] = 0;
+    }
+    uint32_t xa = live ? ((xy_in[s] + 1) & 0xFF) : 1, y = live ? (xy_in[s] >> 8) : 0;
+    __syncthreads();
+
+    const uint32_t m0 = mask_lt(l + 1, 0), m1 = mask_lt(l + 1, 1), m2 = mask_lt(l + 1, 2), m3 = mask_lt(l + 1, 3);
+    const uint32_t bitl16 = (1u << l) | 0x10000u, l1 = (l + 1) << 8;
+    const uint32_t sb = (uint32_t)(uintptr_t)S, mb = (uint32_t)(uintptr_t)M, rb = (uint32_t)(uintptr_t)R;
+    uint32_t V = (1u << 8) | (255 - l);
+    uint32_t rem = live ? (uint32_t)N : 0u, rp = l;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    asm volatile(
+        // prologue: no previous window (empty commit mask, y' = y)
+        "s_mov_b64 s[46:47], 0\n\t"
+        "v_mov_b32 v120, %[y]\n\t"
+        "s_mov_b64 s[44:45], 0\n\t"
+        "WIN_LOOP_%=:\n\t"
+        // window n reads
+        "v_and_b32 v105, 0xfc, %[xa]\n\t"
+        "v_add_u32 v105, %[sb], v105\n\t"
+        "v_add3_u32 v106, %[sb], %[xa], %[l]\n\t"
+        "ds_read2_b32 v[100:101], v105 offset1:1\n\t"
+        "ds_read2_b32 v[102:103], v105 offset0:2 offset1:3\n\t"
+        "ds_read_b32 v104, v105 offset:16\n\t"
+        "ds_read_u8 v107, v106\n\t"
+        // window n-1 tail
+        WIN_TAIL
+        "s_waitcnt lgkmcnt(0)\n\t"
+        // prefix: J = y + a_0 + ... + a_l
+        "v_alignbyte_b32 v108, v101, v100, %[xa]\n\t"
+        "v_alignbyte_b32 v109, v102, v101, %[xa]\n\t"
+        "v_alignbyte_b32 v110, v103, v102, %[xa]\n\t"
+        "v_alignbyte_b32 v111, v104, v103, %[xa]\n\t"
+        "v_and_b32 v108, v108, %[m0]\n\t"
+        "v_and_b32 v110, v110, %[m2]\n\t"
+        "v_and_b32 v109, v109, %[m1]\n\t"
+        "v_and_b32 v111, v111, %[m3]\n\t"
+        "v_sad_u8 v112, v108, 0, %[y]\n\t"
+        "v_sad_u8 v113, v110, 0, 0\n\t"
+        "v_sad_u8 v112, v109, 0, v112\n\t"
+        "v_sad_u8 v113, v111, 0, v113\n\t"
+        "v_add_u32 v112, v112, v113\n\t"
+        "v_and_b32 v112, 0xff, v112\n\t"                       // J (byte)
+        "v_add_u32 v114, %[sb], v112\n\t"                       // &S[J]
+        "v_lshl_add_u32 v115, v112, 2, %[mb]\n\t"               // &M[J]
+        "ds_read_u8 v116, v114\n\t"                             // b
+        "ds_max_u32 v115, %[v]\n\t"
+        "ds_read_b32 v117, v115\n\t"                            // marker winner
+        // rule on d = J - x - 1 (under the round trip)
+        "v_sub_u32 v118, v112, %[xa]\n\t"
+        "v_and_b32 v118, 0xff, v118\n\t"
+        "v_med3_u32 v118, v118, %[l], 16\n\t"
+        "v_lshlrev_b32 v118, v118, 1\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ne_u32 vcc, v117, %[v]\n\t"
+        "v_cndmask_b32 v119, %[c16], %[bitl16], vcc\n\t"
+        "v_and_or_b32 v118, v118, -2, v119\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp v118, v118, v118 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp v118, v118, v118 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp v118, v118, v118 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp v118, v118, v118 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "v_add3_u32 v126, %[sb], v107, v116\n\t"                // &S[a + b] (doubled S: no wrap)
+        "ds_read_u8 v121, v126\n\t"                             // k0 = S0[t]
+        "v_ffbl_b32 v118, v118\n\t"
+        "v_min_u32 v118, v118, %[rem]\n\t"                      // cut
+        "v_cmp_lt_u32 vcc, %[l], v118\n\t"
+        "s_and_saveexec_b64 s[40:41], vcc\n\t"
+        "s_mov_b64 s[46:47], exec\n\t"
+        "v_xor_b32 v127, 0x100, v106\n\t"
+        "ds_write_b8 v106, v116\n\t"                            // S[i] = b, both copies
+        "ds_write_b8 v127, v116\n\t"
+        "ds_write_b8 v114, v107\n\t"                            // S[J] = a, both copies
+        "ds_write_b8 v114, v107 offset:256\n\t"
+        "s_mov_b64 exec, s[40:41]\n\t"
+        "ds_read_u8 v122, v126\n\t"                             // k1 = S_final[t]
+        "v_add_u32 v128, v107, v116\n\t"
+        "v_and_b32 v128, 0xff, v128\n\t"                        // t
+        "v_lshl_add_u32 v129, v128, 2, %[mb]\n\t"
+        "ds_read_b32 v123, v129\n\t"                            // marker of t
+        "v_sub_u32 v128, v128, %[xa]\n\t"
+        "v_and_b32 v128, 0xff, v128\n\t"
+        "v_cmp_le_u32_e64 s[44:45], v128, %[l]\n\t"             // t is an i of a step <= l
+        "v_bfi_b32 v125, %[rmask], %[rp], %[rb]\n\t"            // ring slot of this lane
+        "v_or_b32 v130, %[l1], v112\n\t"
+        "v_cndmask_b32 v120, %[y], v130, vcc\n\t"               // y' candidate
+        "v_add_u32 %[xa], %[xa], v118\n\t"
+        "v_and_b32 %[xa], 0xff, %[xa]\n\t"
+        "v_add_u32 %[rp], %[rp], v118\n\t"
+        "v_sub_u32 %[rem], %[rem], v118\n\t"
+        "v_cmp_ne_u32 vcc, 0, %[rem]\n\t"
+        "s_cbranch_vccnz WIN_LOOP_%=\n\t"
+        WIN_TAIL
+        "s_waitcnt lgkmcnt(0)\n\t"
+        : [xa] "+v"(xa), [y] "+v"(y), [v] "+v"(V), [rem] "+v"(rem), [rp] "+v"(rp)
+        : [l] "v"(l), [sb] "v"(sb), [mb] "v"(mb), [rb] "v"(rb), [m0] "v"(m0), [m1] "v"(m1), [m2] "v"(m2),
+          [m3] "v"(m3), [bitl16] "v"(bitl16), [l1] "v"(l1), [rmask] "s"((uint32_t)(MAXN - 1)), [tailcnt] "n"(4), [c16] "v"(0x10000u)
+        : "memory", "vcc", "scc", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",
+          "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",
+          "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "s40", "s41", "s42", "s43", "s44",
+          "s45", "s46", "s47");
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((xa - 1) & 255) | ((y & 255) << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = (V >> 8) - 2;
+        }
+    }
+}
+
 static void ksa(uint8_t *S, const uint8_t *key, int kl)
 {
     for (int i = 0; i < 256; ++i) S[i] = (uint8_t)i;
@@ -286,7 +452,8 @@ static void run(int ns, int N, int reps)
     std::vector<float> ms;
     for (int r = 0; r < reps; ++r) {
         CHECK(hipEventRecord(e0));
-        if (V3) win3_kernel<W, WPB><<<blocks, 64 * WPB>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        if (V3 == 2) win4_kernel<WPB><<<blocks, 64 * WPB>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if (V3) win3_kernel<W, WPB><<<blocks, 64 * WPB>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else win_kernel<W, WPB><<<blocks, 64 * WPB>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
@@ -328,7 +495,8 @@ int main(int argc, char **argv)
     const int wpb = argc > 4 ? atoi(argv[4]) : 1;
     if (N > MAXN || N % 16) { printf("bytes must be a multiple of 16 and <= %d\n", MAXN); return 1; }
     const int v3 = argc > 5 ? atoi(argv[5]) : 1;
-    if (v3) { if (w == 8) run<8, 1, 1>(ns, N, 20); else if (wpb == 1) run<16, 1, 1>(ns, N, 20); else run<16, 2, 1>(ns, N, 20); }
+    if (v3 == 2) { if (wpb == 1) run<16, 1, 2>(ns, N, 20); else run<16, 2, 2>(ns, N, 20); }
+    else if (v3) { if (w == 8) run<8, 1, 1>(ns, N, 20); else if (wpb == 1) run<16, 1, 1>(ns, N, 20); else run<16, 2, 1>(ns, N, 20); }
     else if (w == 8) { if (wpb == 1) run<8, 1, 0>(ns, N, 20); else run<8, 2, 0>(ns, N, 20); }
     else { if (wpb == 1) run<16, 1, 0>(ns, N, 20); else run<16, 2, 0>(ns, N, 20); }
     return 0;
