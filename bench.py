@@ -322,11 +322,15 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
     }
 
 
+WIN_MAX_GROUPS = 16   # zrc4.hip ZRC4_WIN_MAX_GROUPS
+
+
 def kernel_name(S: int, ids: str = "range") -> str:
     """The kernel the bench's crypt call launches for S sessions (zrc4.hip
-    launch_crypt): more 256-session groups than CUs -> the persistent
-    throughput kernel, otherwise one group per workgroup; grouped ids always
-    take crypt_kernel<kGrouped>."""
+    launch_crypt): at most WIN_MAX_GROUPS aligned groups -> 16 lanes per
+    stream (crypt_win_kernel); more 256-session groups than CUs -> the
+    persistent throughput kernel, otherwise one group per workgroup; grouped
+    ids always take crypt_kernel<kGrouped>."""
     if ids == "grouped":
         return "zrc4::crypt_kernel<2, false>"
     try:
@@ -335,6 +339,8 @@ def kernel_name(S: int, ids: str = "range") -> str:
     except Exception:
         cus = 256
     groups = -(-S // 256)
+    if ids == "range" and groups <= WIN_MAX_GROUPS:
+        return "zrc4::crypt_win_kernel"
     if ids == "range" and 2 * groups <= cus:
         return "zrc4::crypt_half_kernel<false>"
     if ids == "scattered":

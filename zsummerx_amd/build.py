@@ -33,7 +33,7 @@ FRAME_DEPS = FRAME_SOURCES + [ROOT / "include" / "zsummerx_amd" / "frame.h",
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
 HIP_SOURCES = [CSRC / "zrc4.hip"]
-HIP_DEPS = HIP_SOURCES + [CSRC / "zrc4_kernels.hpp", CSRC / "zrc4_line_loop.inc", CSRC / "zrc4_ks.inc",
+HIP_DEPS = HIP_SOURCES + [CSRC / "zrc4_kernels.hpp", CSRC / "zrc4_win.hpp", CSRC / "zrc4_line_loop.inc", CSRC / "zrc4_ks.inc",
                          ROOT / "include" / "zrc4.h"]
 
 
@@ -77,12 +77,13 @@ def build_variant(name: str, defines: dict, rev: str | None = None) -> Path:
         (tree / "include").mkdir(parents=True, exist_ok=True)
         for rel, dst in (("zsummerx_amd/csrc/zrc4.hip", tree / "csrc" / "zrc4.hip"),
                          ("zsummerx_amd/csrc/zrc4_kernels.hpp", tree / "csrc" / "zrc4_kernels.hpp"),
+                         ("zsummerx_amd/csrc/zrc4_win.hpp", tree / "csrc" / "zrc4_win.hpp"),
                          ("zsummerx_amd/csrc/zrc4_line_loop.inc", tree / "csrc" / "zrc4_line_loop.inc"),
                          ("zsummerx_amd/csrc/zrc4_ks.inc", tree / "csrc" / "zrc4_ks.inc"),
                          ("include/zrc4.h", tree / "include" / "zrc4.h")):
             got = subprocess.run(["git", "show", f"{rev}:{rel}"], cwd=ROOT, capture_output=True)
             if got.returncode != 0:
-                if rel.endswith(".inc"):        # older revisions have no generated loop
+                if rel.endswith((".inc", "zrc4_win.hpp")):   # older revisions lack these
                     continue
                 got.check_returncode()
             blob = got.stdout

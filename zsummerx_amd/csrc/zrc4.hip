@@ -5,6 +5,7 @@
 // (include/zsummerX/frame/session.h:115-116); see INTEGRATION.md.
 #include "zrc4.h"
 #include "zrc4_kernels.hpp"
+#include "zrc4_win.hpp"
 
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
@@ -15,6 +16,10 @@
 
 #ifndef ZRC4_HALF
 #define ZRC4_HALF 1   // A/B knob: 0 runs few-group range batches on whole-group workgroups too
+#endif
+#ifndef ZRC4_WIN_MAX_GROUPS
+#define ZRC4_WIN_MAX_GROUPS 16   // aligned range batches of at most this many groups run 16 lanes per
+                                 // stream (crypt_win_kernel, zrc4_win.hpp); 0 = never
 #endif
 
 struct zrc4_ctx {
@@ -91,6 +96,13 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
     const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
     const dim3 blk(zrc4::kGroup);
     const bool stream_kernel = mode != zrc4::kGrouped && grid > (uint32_t)c->num_cus;
+    // Few aligned groups: 16 lanes per stream (speculative windows), one wave
+    // per 4 streams, 64 workgroups per group.
+    if (!fr && mode == zrc4::kRange && (first_slot & 255u) == 0u && grid <= (uint32_t)ZRC4_WIN_MAX_GROUPS) {
+        hipLaunchKernelGGL(zrc4::crypt_win_kernel, dim3(64u * grid), dim3(64), 0, s, c->arena, c->xy, first_slot,
+                           payload, off, len, n);
+        return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
+    }
     // Few whole groups: half-group workgroups, one per CU (2 waves per CU).
     // A grouped bucket's slots may sit in either half whatever its entry
     // count, so it always gets both halves.

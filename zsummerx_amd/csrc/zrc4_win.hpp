@@ -1,0 +1,285 @@
+// zrc4_win.hpp -- lane-parallel speculative RC4 windows for chain-bound launches.
+//
+// Reference: /root/reference/depends/rc4/rc4_encryption.h:81-89 (the PRGA).
+//
+// The lane-per-stream kernels (zrc4_kernels.hpp) run one PRGA step per lane
+// per ~96 cycles: one LDS round trip plus the step's issue.  A launch with few
+// sessions (4 096 x 1 KiB = 16 groups, 1 024 x 64 KiB = 4 groups) leaves most
+// of the chip idle at that per-stream rate.  Here W = 16 lanes run one stream:
+// each lane takes one step of a window of 16 from the window-start state, and
+// the window commits the longest prefix that provably equals the serial order
+// (tools/window_sim.py states and checks the rules):
+//
+//   i_l = x+1+l, a_l = S0[i_l], j_l = y + a_0 + .. + a_l, b_l = S0[j_l],
+//   d_l = (j_l - x - 1) mod 256
+//   d_l < l           -> b_l read a byte an earlier step swapped   -> cut <= l
+//   l < d_l < 16      -> step l swaps a later step's i              -> cut <= d_l
+//   j_k == j_l, k < l -> b_l read a byte step k swapped             -> cut <= l
+//
+// Committed steps touch pairwise distinct bytes, so their swaps are written in
+// parallel; keystream byte l is S_final[t_l] if a committed step <= l wrote
+// t_l = a_l + b_l, else S0[t_l].  About 10 bytes commit per window.
+//
+// One 64-thread workgroup = one wave = 4 streams x 16 lanes.  Per stream in
+// LDS: the S-box twice (bytes p and p + 256 always written together, so the
+// 16-byte window never wraps: 5 aligned dwords), a 256-entry marker table
+// (ds_max of (window tag << 8) | (255 - l): the read-back names the lowest lane
+// whose j hit that byte this window -> the duplicate-j rule and the keystream
+// rule), and a keystream ring of kWinRing bytes.  Payload is XORed from the
+// ring per chunk of kWinRing bytes, loads issued a chunk ahead.
+//
+// Arena access: the 4 streams of a workgroup are the 4 slots whose S-box
+// bytes share one dword of every image row (col bits 0-1 = lane >> 5,
+// wave & 1, see col_of), so the state moves as 256 aligned dword loads and
+// stores per workgroup: slots g*256 + 128h + L + 32b, b = 0..3, for dword
+// column q = 32h + L.
+#pragma once
+#include "zrc4_kernels.hpp"
+
+namespace zrc4 {
+
+constexpr uint32_t kWinLanes = 16;           // W: lanes (steps) per stream window
+constexpr uint32_t kWinStreams = 4;          // streams per wave / workgroup
+constexpr uint32_t kWinRing = 2048;          // keystream chunk per stream (bytes)
+constexpr uint32_t kWinUnits = kWinRing / 16 / kWinLanes;   // 16-byte payload units per lane per chunk
+
+__device__ __forceinline__ uint32_t win_mask_lt(uint32_t c, uint32_t q)   // bytes k < c of dword q
+{
+    return c <= 4 * q ? 0u : (c >= 4 * q + 4 ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (32 - 8 * (c - 4 * q))));
+}
+
+// Tail of window n-1, run under window n's read round trip: y' = J of the last
+// committed lane (DPP max over the 16 lanes of (l + 1) << 8 | J, or the old y),
+// the keystream select (S_final if a committed step <= l wrote t, else S0) and
+// the ring store of committed lanes.
+#define ZRC4_WIN_TAIL                                                                             \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v120, v120, v120 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"           \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v120, v120, v120 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"           \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v120, v120, v120 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"               \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v120, v120, v120 row_mirror row_mask:0xf bank_mask:0xf\n\t"                    \
+    "s_waitcnt lgkmcnt(4)\n\t"                                                                    \
+    "v_cmp_ge_u32_e64 s[42:43], v123, %[v]\n\t"                                                   \
+    "s_or_b64 s[42:43], s[42:43], s[44:45]\n\t"                                                   \
+    "v_cndmask_b32_e64 v124, v121, v122, s[42:43]\n\t"                                            \
+    "s_mov_b64 s[40:41], exec\n\t"                                                                \
+    "s_mov_b64 exec, s[46:47]\n\t"                                                                \
+    "ds_write_b8 v125, v124\n\t"                                                                  \
+    "s_mov_b64 exec, s[40:41]\n\t"                                                                \
+    "v_and_b32 %[y], 0xff, v120\n\t"                                                              \
+    "v_add_u32 %[v], 0x100, %[v]\n\t"
+
+struct WinLane {
+    uint32_t xa;     // x + 1 (byte)
+    uint32_t y;      // y (byte)
+    uint32_t v;      // marker value: window tag << 8 | (255 - l)
+    uint32_t rp;     // stream position + l (ring slot before masking)
+};
+
+// Windows until every stream of the wave has consumed `rem` bytes (rem is per
+// lane, equal inside a stream's 16 lanes; 0 = idle).  One asm statement:
+// reads of window n issue first; the tail of window n-1 runs under their
+// round trip; prefix (alignbyte, and, sad) -> b and marker reads -> the d rule
+// under that round trip -> the duplicate rule -> DPP OR -> cut -> S0[t] read
+// -> commit (both S copies) -> S_final[t] and marker(t) reads -> updates.
+// Pinned temporaries v100-v130, s[40:47].
+__device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l, uint32_t sb, uint32_t mb,
+                                            uint32_t rb, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3)
+{
+    const uint32_t bitl16 = (1u << l) | 0x10000u, l1 = (l + 1) << 8;
+    asm volatile(
+        "s_mov_b64 s[46:47], 0\n\t"
+        "v_mov_b32 v120, %[y]\n\t"
+        "s_mov_b64 s[44:45], 0\n\t"
+        "ZW_LOOP_%=:\n\t"
+        "v_and_b32 v105, 0xfc, %[xa]\n\t"
+        "v_add_u32 v105, %[sb], v105\n\t"
+        "v_add3_u32 v106, %[sb], %[xa], %[l]\n\t"
+        "ds_read2_b32 v[100:101], v105 offset1:1\n\t"
+        "ds_read2_b32 v[102:103], v105 offset0:2 offset1:3\n\t"
+        "ds_read_b32 v104, v105 offset:16\n\t"
+        "ds_read_u8 v107, v106\n\t"                             // a_l
+        ZRC4_WIN_TAIL
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_alignbyte_b32 v108, v101, v100, %[xa]\n\t"
+        "v_alignbyte_b32 v109, v102, v101, %[xa]\n\t"
+        "v_alignbyte_b32 v110, v103, v102, %[xa]\n\t"
+        "v_alignbyte_b32 v111, v104, v103, %[xa]\n\t"
+        "v_and_b32 v108, v108, %[m0]\n\t"
+        "v_and_b32 v110, v110, %[m2]\n\t"
+        "v_and_b32 v109, v109, %[m1]\n\t"
+        "v_and_b32 v111, v111, %[m3]\n\t"
+        "v_sad_u8 v112, v108, 0, %[y]\n\t"
+        "v_sad_u8 v113, v110, 0, 0\n\t"
+        "v_sad_u8 v112, v109, 0, v112\n\t"
+        "v_sad_u8 v113, v111, 0, v113\n\t"
+        "v_add_u32 v112, v112, v113\n\t"
+        "v_and_b32 v112, 0xff, v112\n\t"                       // j_l
+        "v_add_u32 v114, %[sb], v112\n\t"
+        "v_lshl_add_u32 v115, v112, 2, %[mb]\n\t"
+        "ds_read_u8 v116, v114\n\t"                             // b_l = S0[j_l]
+        "ds_max_u32 v115, %[v]\n\t"
+        "ds_read_b32 v117, v115\n\t"                            // lowest lane with this j
+        "v_sub_u32 v118, v112, %[xa]\n\t"
+        "v_and_b32 v118, 0xff, v118\n\t"
+        "v_med3_u32 v118, v118, %[l], 16\n\t"                   // d < l -> l, l <= d < 16 -> d, else 16
+        "v_lshlrev_b32 v118, v118, 1\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ne_u32 vcc, v117, %[v]\n\t"
+        "v_cndmask_b32 v119, %[c16], %[bitl16], vcc\n\t"
+        "v_and_or_b32 v118, v118, -2, v119\n\t"                // lane 0 never cuts at 0
+        "s_nop 1\n\t"
+        "v_or_b32_dpp v118, v118, v118 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp v118, v118, v118 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp v118, v118, v118 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp v118, v118, v118 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "v_add3_u32 v126, %[sb], v107, v116\n\t"                // &S[a + b]: the doubled S wraps for free
+        "ds_read_u8 v121, v126\n\t"                             // S0[t]
+        "v_ffbl_b32 v118, v118\n\t"
+        "v_min_u32 v118, v118, %[rem]\n\t"                      // cut
+        "v_cmp_lt_u32 vcc, %[l], v118\n\t"
+        "s_and_saveexec_b64 s[40:41], vcc\n\t"
+        "s_mov_b64 s[46:47], exec\n\t"
+        "v_xor_b32 v127, 0x100, v106\n\t"
+        "ds_write_b8 v106, v116\n\t"                            // S[i_l] = b_l, both copies
+        "ds_write_b8 v127, v116\n\t"
+        "ds_write_b8 v114, v107\n\t"                            // S[j_l] = a_l, both copies
+        "ds_write_b8 v114, v107 offset:256\n\t"
+        "s_mov_b64 exec, s[40:41]\n\t"
+        "ds_read_u8 v122, v126\n\t"                             // S_final[t]
+        "v_add_u32 v128, v107, v116\n\t"
+        "v_and_b32 v128, 0xff, v128\n\t"
+        "v_lshl_add_u32 v129, v128, 2, %[mb]\n\t"
+        "ds_read_b32 v123, v129\n\t"                            // lowest lane whose j == t
+        "v_sub_u32 v128, v128, %[xa]\n\t"
+        "v_and_b32 v128, 0xff, v128\n\t"
+        "v_cmp_le_u32_e64 s[44:45], v128, %[l]\n\t"             // t is the i of a step <= l
+        "v_bfi_b32 v125, %[rmask], %[rp], %[rb]\n\t"            // ring slot
+        "v_or_b32 v130, %[l1], v112\n\t"
+        "v_cndmask_b32 v120, %[y], v130, vcc\n\t"
+        "v_add_u32 %[xa], %[xa], v118\n\t"
+        "v_and_b32 %[xa], 0xff, %[xa]\n\t"
+        "v_add_u32 %[rp], %[rp], v118\n\t"
+        "v_sub_u32 %[rem], %[rem], v118\n\t"
+        "v_cmp_ne_u32 vcc, 0, %[rem]\n\t"
+        "s_cbranch_vccnz ZW_LOOP_%=\n\t"
+        ZRC4_WIN_TAIL
+        "s_waitcnt lgkmcnt(0)\n\t"
+        : [xa] "+v"(w.xa), [y] "+v"(w.y), [v] "+v"(w.v), [rem] "+v"(rem), [rp] "+v"(w.rp)
+        : [l] "v"(l), [sb] "v"(sb), [mb] "v"(mb), [rb] "v"(rb), [m0] "v"(m0), [m1] "v"(m1), [m2] "v"(m2),
+          [m3] "v"(m3), [bitl16] "v"(bitl16), [l1] "v"(l1), [rmask] "s"(kWinRing - 1), [c16] "v"(0x10000u)
+        : "memory", "vcc", "scc", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",
+          "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",
+          "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "s40", "s41", "s42", "s43", "s44",
+          "s45", "s46", "s47");
+}
+
+// Range batches with first_slot % 256 == 0 and few groups: grid = 64 x groups
+// workgroups of one wave.  Workgroup k -> (group, dword column) with the 8
+// columns of one XCD (k mod 8) adjacent, so a row's image bytes are shared by
+// few L2s.
+__global__ void __launch_bounds__(64)
+crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uint32_t first_slot,
+                 uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
+                 const uint32_t *__restrict__ len, uint32_t n)
+{
+    __shared__ __attribute__((aligned(1024))) uint32_t Mk[kWinStreams * 256];
+    __shared__ __attribute__((aligned(kWinRing))) uint8_t Ring[kWinStreams * kWinRing];
+    __shared__ __attribute__((aligned(512))) uint8_t Sb[kWinStreams * 512];
+
+    const uint32_t k = blockIdx.x, xcd = k & 7u, idx = k >> 3;
+    const uint32_t q = (idx & 7u) | (xcd << 3), g = idx >> 3;
+    const uint32_t lane = threadIdx.x, l = lane & 15u, b = lane >> 4;
+    const uint32_t e = g * kGroup + ((q >> 5) << 7) + (q & 31u) + 32u * b;   // entry of this lane's stream
+    const uint32_t slot = first_slot + e;
+    const bool valid = e < n;
+    if (!__builtin_amdgcn_ballot_w64(valid)) return;                          // whole dword column idle
+
+    uint8_t *img = arena + (size_t)(slot >> 8) * kGroupBytes + 4u * q;      // + row * 256
+    uint32_t rows[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
+    const uint32_t L = valid ? len[e] : 0u;
+    const uint64_t O = valid ? off[e] : 0u;
+    const uint32_t sxy = valid ? xy[slot] : 0u;
+    uint8_t *msg = payload + O;
+    const bool aligned = ((uintptr_t)msg & 15u) == 0u;
+
+    // payload prefetch of chunk 0 (aligned messages: whole 16-byte units)
+    uint4 pre[kWinUnits];
+#pragma unroll
+    for (uint32_t u = 0; u < kWinUnits; ++u) {
+        const uint32_t pos = 16u * (l + kWinLanes * u);
+        if (aligned && pos + 16u <= L) pre[u] = *reinterpret_cast<const uint4 *>(msg + pos);
+    }
+
+    uint8_t *S = Sb + b * 512u;
+    uint32_t *M = Mk + b * 256u;
+    uint8_t *R = Ring + b * kWinRing;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t kk = lane + 64u * r;
+#pragma unroll
+        for (uint32_t s4 = 0; s4 < 4; ++s4) {
+            const uint8_t v = (uint8_t)(rows[r] >> (8 * s4));
+            Sb[s4 * 512u + kk] = v;
+            Sb[s4 * 512u + 256u + kk] = v;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) reinterpret_cast<uint4 *>(Mk)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+
+    const uint32_t m0 = win_mask_lt(l + 1, 0), m1 = win_mask_lt(l + 1, 1), m2 = win_mask_lt(l + 1, 2),
+                   m3 = win_mask_lt(l + 1, 3);
+    const uint32_t sb = (uint32_t)(uintptr_t)S, mb = (uint32_t)(uintptr_t)M, rb = (uint32_t)(uintptr_t)R;
+    WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
+
+    for (uint32_t c0 = 0; __builtin_amdgcn_ballot_w64(c0 < L); c0 += kWinRing) {
+        const uint32_t c1 = L < c0 + kWinRing ? L : c0 + kWinRing;
+        const uint32_t rem = c0 < L ? c1 - c0 : 0u;
+        win_windows(w, rem, l, sb, mb, rb, m0, m1, m2, m3);
+        // XOR pass of [c0, c1): whole 16-byte units from the prefetch, bytes otherwise
+        if (aligned) {
+#pragma unroll
+            for (uint32_t u = 0; u < kWinUnits; ++u) {
+                const uint32_t pos = c0 + 16u * (l + kWinLanes * u);
+                if (pos + 16u <= c1) {
+                    const uint4 ks = *reinterpret_cast<const uint4 *>(R + (pos & (kWinRing - 1u)));
+                    uint4 v = pre[u];
+                    v.x ^= ks.x; v.y ^= ks.y; v.z ^= ks.z; v.w ^= ks.w;
+                    *reinterpret_cast<uint4 *>(msg + pos) = v;
+                }
+            }
+            for (uint32_t pos = c0 + ((c1 - c0) & ~15u) + l; pos < c1; pos += kWinLanes)   // ragged tail
+                msg[pos] ^= R[pos & (kWinRing - 1u)];
+        } else {
+            for (uint32_t pos = c0 + l; pos < c1; pos += kWinLanes) msg[pos] ^= R[pos & (kWinRing - 1u)];
+        }
+        // prefetch of the next chunk
+        const uint32_t n0 = c0 + kWinRing;
+#pragma unroll
+        for (uint32_t u = 0; u < kWinUnits; ++u) {
+            const uint32_t pos = n0 + 16u * (l + kWinLanes * u);
+            if (aligned && pos + 16u <= L) pre[u] = *reinterpret_cast<const uint4 *>(msg + pos);
+        }
+    }
+
+    if (valid && l == 0) xy[slot] = (uint16_t)(((w.xa - 1u) & 0xFFu) | ((w.y & 0xFFu) << 8));
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t kk = lane + 64u * r;
+        const uint32_t v = (uint32_t)Sb[kk] | ((uint32_t)Sb[512u + kk] << 8) | ((uint32_t)Sb[1024u + kk] << 16) |
+                           ((uint32_t)Sb[1536u + kk] << 24);
+        *reinterpret_cast<uint32_t *>(img + (size_t)kk * 256u) = v;
+    }
+}
+
+}  // namespace zrc4
