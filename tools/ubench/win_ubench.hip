@@ -417,12 +417,10 @@ win6_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint
     }
     const uint32_t sxy = live ? xy_in[s] : 0;
     __syncthreads();
-    const uint32_t m0 = zrc4::win_mask_lt(l + 1, 0), m1 = zrc4::win_mask_lt(l + 1, 1),
-                   m2 = zrc4::win_mask_lt(l + 1, 2), m3 = zrc4::win_mask_lt(l + 1, 3);
     zrc4::WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     zrc4::win_windows(w, live ? (uint32_t)N : 0u, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
-                      (uint32_t)(uintptr_t)R, m0, m1, m2, m3);
+                      (uint32_t)(uintptr_t)R);
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     __syncthreads();
     if (live) {

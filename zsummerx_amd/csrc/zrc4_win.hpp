@@ -21,8 +21,8 @@
 // t_l = a_l + b_l, else S0[t_l].  About 10 bytes commit per window.
 //
 // One 64-thread workgroup = one wave = 4 streams x 16 lanes.  Per stream in
-// LDS: the S-box twice (bytes p and p + 256 always written together, so the
-// 16-byte window never wraps: 5 aligned dwords), a 256-entry marker table
+// LDS: the S-box twice (bytes p and p + 256 always written together, so
+// S[x + 1 + l] and S[a + b] need no wrap), a 256-entry marker table
 // (ds_max of (window tag << 8) | (255 - l): the read-back names the lowest lane
 // whose j hit that byte this window -> the duplicate-j rule and the keystream
 // rule), and a keystream ring of kWinRing bytes.  Payload is XORed from the
@@ -43,11 +43,6 @@ constexpr uint32_t kWinStreams = 4;          // streams per wave / workgroup
 constexpr uint32_t kWinRing = 2048;          // keystream chunk per stream (bytes)
 constexpr uint32_t kWinUnits = kWinRing / 16 / kWinLanes;   // 16-byte payload units per lane per chunk
 
-__device__ __forceinline__ uint32_t win_mask_lt(uint32_t c, uint32_t q)   // bytes k < c of dword q
-{
-    return c <= 4 * q ? 0u : (c >= 4 * q + 4 ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (32 - 8 * (c - 4 * q))));
-}
-
 struct WinLane {
     uint32_t xa;     // x + 1 (byte)
     uint32_t y;      // y (byte)
@@ -56,27 +51,55 @@ struct WinLane {
 };
 
 // Windows until every stream of the wave has consumed `rem` bytes (rem is per
-// lane, equal inside a stream's 16 lanes; 0 = idle).  One asm statement, per
-// window n:
-//   1. the window's 5 dwords and a_l are read;
-//   2. under that round trip, window n-1's tail: y' = J of its last committed
-//      lane (DPP max over the 16 lanes of (l + 1) << 8 | J, else the old y),
-//      its keystream select (S_final if a committed step <= l wrote t, else
-//      S0) and ring store;
-//   3. J_l = y + a_0 + .. + a_l (alignbyte, and, sad);
-//      b_l = S0[J_l] and the marker max/read-back issue;
-//   4. under that round trip, the d rule (one-hot of med3(d, l, 16), none
-//      when d == l);
-//   5. the duplicate-j rule, DPP OR over the 16 lanes with the keystream
-//      address work in the DPP wait slots, cut = lowest bit (<= rem);
-//   6. S0[t] was read before, the commit (4 byte writes, both S copies) under
-//      exec = lanes < cut, S_final[t] and marker(t) reads, updates.
-// Pinned temporaries v100-v131, s[40:47].  m0..m3: 0xFF in bytes k <= l.
-// (v_dot4_u32_u8 against 0/1 masks would save the four ands, but a dot4 chain
-// read its accumulator stale on MI355X -- bit-exact only because the wrong j
-// always tripped the duplicate rule -- so the known VALU path stays.)
+// lane, equal inside a stream's 16 lanes; 0 = idle).  One asm statement; the
+// loop is rotated so that window n+1's read leaves right behind window n's
+// commit writes.  Per iteration n (a_l of window n already in flight):
+//   1. two interleaved DPP chains: the inclusive scan of a over the stream's
+//      16 lanes (row_shr 1, 2, 4, 8: J_l = y + a_0 + .. + a_l) and window
+//      n-1's y' = J of its last committed lane (max over the 16 lanes of
+//      (l + 1) << 8 | J, else the old y); window n-1's keystream select
+//      (S_final if a committed step <= l wrote t, else S0) and ring store fill
+//      the DPP wait slots;
+//   2. b_l = S0[J_l] and the marker max / read-back issue; under that round
+//      trip the d rule (one-hot of med3(d, l, 16), none when d == l);
+//   3. the duplicate-j rule, DPP OR over the 16 lanes with the keystream
+//      address work and S0[t] read in the DPP wait slots, cut = lowest bit
+//      (<= rem), x and window n+1's a_l address;
+//   4. commit (4 byte writes, both S copies) under exec = lanes < cut, window
+//      n+1's a_l read, S_final[t] and marker(t) reads, updates.
+// Every DPP read of a VGPR sits at least two VALU ops (or an s_nop) after the
+// VALU write of it.  Pinned temporaries v106-v131, s[40:47].
+// (v_dot4_u32_u8 prefix sums over the window bytes were tried: the dot4
+// accumulator chain read stale values on MI355X -- bit-exact only because the
+// wrong j always tripped the duplicate rule -- and the DPP scan needs no
+// window bytes at all.)
+#define ZW_TAIL_SCAN(SCAN)                                                                        \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
+    "v_mov_b32 v112, v107\n\t"                                                                    \
+    "v_max_u32_dpp v120, v120, v120 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"           \
+    "v_cmp_ge_u32_e64 s[42:43], v123, %[v]\n\t"                                                   \
+    SCAN("row_shr:1")                                                                             \
+    "v_xor_b32 v127, 0x100, v106\n\t"                                                             \
+    "v_max_u32_dpp v120, v120, v120 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"           \
+    "s_or_b64 s[42:43], s[42:43], s[44:45]\n\t"                                                   \
+    "v_cndmask_b32_e64 v124, v121, v122, s[42:43]\n\t"                                            \
+    SCAN("row_shr:2")                                                                             \
+    "v_add_u32 %[v], 0x100, %[v]\n\t"                                                             \
+    "v_max_u32_dpp v120, v120, v120 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"               \
+    "s_mov_b64 s[40:41], exec\n\t"                                                                \
+    "s_nop 0\n\t"                                                                                 \
+    SCAN("row_shr:4")                                                                             \
+    "s_mov_b64 exec, s[46:47]\n\t"                                                                \
+    "ds_write_b8 v125, v124\n\t"                                                                  \
+    "s_mov_b64 exec, s[40:41]\n\t"                                                                \
+    "v_max_u32_dpp v120, v120, v120 row_mirror row_mask:0xf bank_mask:0xf\n\t"                    \
+    "s_nop 1\n\t"                                                                                 \
+    SCAN("row_shr:8")
+#define ZW_SCAN(CTRL) "v_add_u32_dpp v112, v112, v112 " CTRL " row_mask:0xf bank_mask:0xf\n\t"
+#define ZW_NOSCAN(CTRL) "s_nop 0\n\t"
+#define ZW_ADDR(XA) "v_add3_u32 v106, %[sb], " XA ", %[l]\n\t"
 __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l, uint32_t sb, uint32_t mb,
-                                            uint32_t rb, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3)
+                                            uint32_t rb)
 {
     const uint32_t bitl = 1u << l, l1 = (l + 1) << 8;
     asm volatile(
@@ -84,54 +107,20 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_and_b32 v120, 0xff, %[y]\n\t"
         "s_mov_b64 s[44:45], 0\n\t"
         "v_mov_b32 v123, 0\n\t"
+        ZW_ADDR("%[xa]")
+        "ds_read_u8 v107, v106\n\t"                             // a_l of window 0
         "ZW_LOOP_%=:\n\t"
-        // 1. window reads
-        "v_and_b32 v105, 0xfc, %[xa]\n\t"
-        "v_add_u32 v105, %[sb], v105\n\t"
-        "v_add3_u32 v106, %[sb], %[xa], %[l]\n\t"               // &S[x + 1 + l] (copy 0 or 1)
-        "ds_read2_b32 v[100:101], v105 offset1:1\n\t"
-        "ds_read2_b32 v[102:103], v105 offset0:2 offset1:3\n\t"
-        "ds_read_b32 v104, v105 offset:16\n\t"
-        "ds_read_u8 v107, v106\n\t"                             // a_l
-        "v_xor_b32 v127, 0x100, v106\n\t"                       // the other copy of S[i_l]
-        // 2. tail of window n-1 (its S_final[t] / marker(t) reads are older than the 4 above)
-        "s_waitcnt lgkmcnt(4)\n\t"
-        "v_max_u32_dpp v120, v120, v120 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_cmp_ge_u32_e64 s[42:43], v123, %[v]\n\t"
-        "s_or_b64 s[42:43], s[42:43], s[44:45]\n\t"
-        "v_max_u32_dpp v120, v120, v120 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-        "v_cndmask_b32_e64 v124, v121, v122, s[42:43]\n\t"
-        "v_add_u32 %[v], 0x100, %[v]\n\t"
-        "v_max_u32_dpp v120, v120, v120 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "s_mov_b64 s[40:41], exec\n\t"
-        "s_nop 0\n\t"
-        "v_max_u32_dpp v120, v120, v120 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "s_mov_b64 exec, s[46:47]\n\t"
-        "ds_write_b8 v125, v124\n\t"                            // ring <- keystream of window n-1
-        "s_mov_b64 exec, s[40:41]\n\t"
+        // 1. scan of a, tail of window n-1
+        ZW_TAIL_SCAN(ZW_SCAN)
         "v_and_b32 %[y], 0xff, v120\n\t"
-        "s_waitcnt lgkmcnt(1)\n\t"                              // window dwords and a_l
-        // 3. J and the round trip for b / marker
-        "v_alignbyte_b32 v108, v101, v100, %[xa]\n\t"
-        "v_alignbyte_b32 v109, v102, v101, %[xa]\n\t"
-        "v_alignbyte_b32 v110, v103, v102, %[xa]\n\t"
-        "v_alignbyte_b32 v111, v104, v103, %[xa]\n\t"
-        "v_and_b32 v108, v108, %[m0]\n\t"
-        "v_and_b32 v110, v110, %[m2]\n\t"
-        "v_and_b32 v109, v109, %[m1]\n\t"
-        "v_and_b32 v111, v111, %[m3]\n\t"
-        "v_sad_u8 v112, v108, 0, %[y]\n\t"
-        "v_sad_u8 v113, v110, 0, 0\n\t"
-        "v_sad_u8 v112, v109, 0, v112\n\t"
-        "v_sad_u8 v113, v111, 0, v113\n\t"
-        "v_add_u32 v112, v112, v113\n\t"
+        "v_add_u32 v112, v112, %[y]\n\t"
+        // 2. b / marker round trip, d rule under it
         "v_add_u32_sdwa v114, %[sb], v112 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"
         "v_and_b32 v112, 0xff, v112\n\t"                       // J
         "v_lshl_add_u32 v115, v112, 2, %[mb]\n\t"
         "ds_read_u8 v116, v114\n\t"                             // b_l = S0[J]
         "ds_max_u32 v115, %[v]\n\t"
         "ds_read_b32 v117, v115\n\t"                            // lowest lane with this J
-        // 4. d rule under the round trip
         "v_sub_u32 v118, v112, %[xa]\n\t"
         "v_and_b32 v118, 0xff, v118\n\t"                       // d
         "v_med3_u32 v119, v118, %[l], 16\n\t"
@@ -139,12 +128,12 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_cndmask_b32 v119, 16, v119, vcc\n\t"
         "v_lshlrev_b32 v118, v119, 1\n\t"                       // bit 16 = no d conflict
         "v_or_b32 v130, %[l1], v112\n\t"                        // y' candidate of this lane
+        "v_bfi_b32 v125, %[rmask], %[rp], %[rb]\n\t"            // ring slot of this lane
         "s_waitcnt lgkmcnt(0)\n\t"
-        // 5. duplicate-J rule, OR over the stream's 16 lanes, cut
+        // 3. duplicate-J rule, OR over the stream's 16 lanes, cut
         "v_cmp_ne_u32 vcc, v117, %[v]\n\t"
         "v_cndmask_b32 v119, 0, %[bitl], vcc\n\t"
         "v_or_b32 v118, v118, v119\n\t"
-        // each DPP read of v118 has two VALU ops (the required wait states) after its write
         "v_add3_u32 v126, %[sb], v107, v116\n\t"                // &S[a + b]: the doubled S wraps for free
         "v_add_u32 v128, v107, v116\n\t"
         "ds_read_u8 v121, v126\n\t"                             // S0[t]
@@ -156,52 +145,40 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_lshl_add_u32 v129, v128, 2, %[mb]\n\t"
         "v_or_b32_dpp v118, v118, v118 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
         "v_cmp_le_u32_e64 s[44:45], v131, %[l]\n\t"             // t is the i of a step <= l
-        "v_bfi_b32 v125, %[rmask], %[rp], %[rb]\n\t"            // ring slot of this lane
+        "v_mov_b32 v131, v106\n\t"                              // &S[i_l] of window n
         "v_or_b32_dpp v118, v118, v118 row_mirror row_mask:0xf bank_mask:0xf\n\t"
         "v_ffbl_b32 v118, v118\n\t"
         "v_min_u32 v118, v118, %[rem]\n\t"                      // cut
-        // 6. commit
+        "v_add_u32 %[xa], %[xa], v118\n\t"
+        "v_and_b32 %[xa], 0xff, %[xa]\n\t"
         "v_cmp_lt_u32 vcc, %[l], v118\n\t"
+        ZW_ADDR("%[xa]")                                        // window n+1's a_l address
+        // 4. commit, then window n+1's read right behind it
         "s_and_saveexec_b64 s[40:41], vcc\n\t"
         "s_mov_b64 s[46:47], exec\n\t"
-        "ds_write_b8 v106, v116\n\t"                            // S[i_l] = b_l, both copies
+        "ds_write_b8 v131, v116\n\t"                            // S[i_l] = b_l, both copies
         "ds_write_b8 v127, v116\n\t"
         "ds_write_b8 v114, v107\n\t"                            // S[J_l] = a_l, both copies
         "ds_write_b8 v114, v107 offset:256\n\t"
         "s_mov_b64 exec, s[40:41]\n\t"
+        "v_cndmask_b32 v120, %[y], v130, vcc\n\t"
+        "ds_read_u8 v107, v106\n\t"                             // a_l of window n+1
         "ds_read_u8 v122, v126\n\t"                             // S_final[t]
         "ds_read_b32 v123, v129\n\t"                            // lowest lane whose J == t
-        "v_add_u32 %[xa], %[xa], v118\n\t"
-        "v_and_b32 %[xa], 0xff, %[xa]\n\t"
         "v_sub_u32 %[rem], %[rem], v118\n\t"
         "v_add_u32 %[rp], %[rp], v118\n\t"
-        "v_cndmask_b32 v120, %[y], v130, vcc\n\t"
         "v_cmp_ne_u32 vcc, 0, %[rem]\n\t"
         "s_cbranch_vccnz ZW_LOOP_%=\n\t"
-        // drain: tail of the last window
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "v_max_u32_dpp v120, v120, v120 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_cmp_ge_u32_e64 s[42:43], v123, %[v]\n\t"
-        "s_or_b64 s[42:43], s[42:43], s[44:45]\n\t"
-        "v_max_u32_dpp v120, v120, v120 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-        "v_cndmask_b32_e64 v124, v121, v122, s[42:43]\n\t"
-        "v_add_u32 %[v], 0x100, %[v]\n\t"
-        "v_max_u32_dpp v120, v120, v120 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "s_mov_b64 s[40:41], exec\n\t"
-        "s_nop 0\n\t"
-        "v_max_u32_dpp v120, v120, v120 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "s_mov_b64 exec, s[46:47]\n\t"
-        "ds_write_b8 v125, v124\n\t"
-        "s_mov_b64 exec, s[40:41]\n\t"
+        // drain: tail of the last window (window n's read is harmless)
+        ZW_TAIL_SCAN(ZW_NOSCAN)
         "v_and_b32 %[y], 0xff, v120\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
         : [xa] "+v"(w.xa), [y] "+v"(w.y), [v] "+v"(w.v), [rem] "+v"(rem), [rp] "+v"(w.rp)
-        : [l] "v"(l), [sb] "v"(sb), [mb] "v"(mb), [rb] "v"(rb), [m0] "v"(m0), [m1] "v"(m1), [m2] "v"(m2),
-          [m3] "v"(m3), [bitl] "v"(bitl), [l1] "v"(l1), [rmask] "s"(kWinRing - 1)
-        : "memory", "vcc", "scc", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",
-          "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",
-          "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "s40", "s41", "s42", "s43",
-          "s44", "s45", "s46", "s47");
+        : [l] "v"(l), [sb] "v"(sb), [mb] "v"(mb), [rb] "v"(rb), [bitl] "v"(bitl), [l1] "v"(l1),
+          [rmask] "s"(kWinRing - 1)
+        : "memory", "vcc", "scc", "v106", "v107", "v112", "v114", "v115", "v116", "v117", "v118", "v119", "v120",
+          "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "s40", "s41",
+          "s42", "s43", "s44", "s45", "s46", "s47");
 }
 
 // Range batches with first_slot % 256 == 0 and few groups: grid = 64 x groups
@@ -260,15 +237,13 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uint32_
     for (int i = 0; i < 4; ++i) reinterpret_cast<uint4 *>(Mk)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
 
-    const uint32_t m0 = win_mask_lt(l + 1, 0), m1 = win_mask_lt(l + 1, 1), m2 = win_mask_lt(l + 1, 2),
-                   m3 = win_mask_lt(l + 1, 3);
     const uint32_t sb = (uint32_t)(uintptr_t)S, mb = (uint32_t)(uintptr_t)M, rb = (uint32_t)(uintptr_t)R;
     WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
 
     for (uint32_t c0 = 0; __builtin_amdgcn_ballot_w64(c0 < L); c0 += kWinRing) {
         const uint32_t c1 = L < c0 + kWinRing ? L : c0 + kWinRing;
         const uint32_t rem = c0 < L ? c1 - c0 : 0u;
-        win_windows(w, rem, l, sb, mb, rb, m0, m1, m2, m3);
+        win_windows(w, rem, l, sb, mb, rb);
         // XOR pass of [c0, c1): whole 16-byte units from the prefetch, bytes otherwise
         if (aligned) {
 #pragma unroll
