@@ -386,6 +386,56 @@ def test_direct_path_block_edges(built, torch_cuda, first_slot):
             assert (sb, x, y) == (bytes(want_sb), wx, wy), i
 
 
+# ------------------------- speculative-window path (crypt_win_kernel, <= 16 groups)
+@pytest.mark.parametrize("first_slot,n", [(0, 16 * 256 - 37), (768, 5)])
+def test_window_path_ragged(built, torch_cuda, first_slot, n):
+    """Aligned range batches of at most 16 groups run 16 lanes per stream
+    (zsummerx_amd/csrc/zrc4_win.hpp).  Lengths 0..5000 including every
+    16-byte edge and messages longer than the 2 KiB keystream chunk (2-3
+    chunks), 16-byte aligned and unaligned message starts (the byte path),
+    untouched gaps, a partial last group (the dword columns of the missing
+    slots must keep their state), three calls in a row (x/y and image
+    write-back), and states checked against the oracle afterwards."""
+    torch = torch_cuda
+    rng = np.random.default_rng(31 + n)
+    keys = rng.integers(0, 256, 16 * n, dtype=np.uint8)
+    koff = np.arange(n, dtype=np.uint64) * 16
+    klen = np.full(n, 16, dtype=np.uint32)
+    ob = pyoracle.Batch(n)
+    ob.make_sbox(keys, koff, klen)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    edges = [0, 1, 15, 16, 17, 31, 32, 33, 255, 256, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4096, 4097, 5000]
+    s = torch.cuda.current_stream()
+    cap = first_slot + -(-n // 256) * 256 + 256
+    with Context(0, cap) as c:
+        c.ksa_range(first_slot, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
+        # a slot outside the batch that shares its image dword with batch slots
+        nslot = first_slot + (n if n > 64 else 33)
+        neighbour = c.get_state(nslot)
+        for call in range(3):
+            L = np.where(rng.random(n) < 0.3, np.resize(edges, n), rng.integers(0, 1500, n)).astype(np.uint32)
+            rng.shuffle(L)
+            lead = np.where(np.arange(n) % 2 == 0, 0, rng.integers(1, 16, n)).astype(np.uint64)
+            gap = (rng.integers(0, 4, n) * 16).astype(np.uint64)
+            seg = ((L.astype(np.uint64) + 15) // 16) * 16 + 16
+            base = np.concatenate([[0], np.cumsum(seg + gap)[:-1]]).astype(np.uint64)
+            off = base + lead
+            data = rng.integers(0, 256, int(base[-1] + seg[-1] + gap[-1]) + 64, dtype=np.uint8)
+            want = data.copy()
+            ob.crypt(want, off, L, threads=8)
+            pay = T(data)
+            c.crypt_range(first_slot, pay, T(off.view(np.int64)), T(L.view(np.int32)), stream=s)
+            c.sync(s)
+            got = pay.cpu().numpy()
+            bad = np.flatnonzero(got != want)
+            assert bad.size == 0, (call, bad[:8], int(bad.size))
+        for i in sorted({0, 1, n // 2, n - 1}):
+            sb, x, y = c.get_state(first_slot + i)
+            want_sb, wx, wy = ob.state(i)
+            assert (sb, x, y) == (bytes(want_sb), wx, wy), i
+        assert c.get_state(nslot) == neighbour
+
+
 # ------------------------------------------ grouped ids (zrc4_crypt_grouped)
 def grouped_batch(rng, n_groups, groups_total, fill=(1, 256)):
     """Buckets of 256 entries: bucket b takes a random subset (random order)

@@ -18,8 +18,8 @@
 #define ZRC4_HALF 1   // A/B knob: 0 runs few-group range batches on whole-group workgroups too
 #endif
 #ifndef ZRC4_WIN_MAX_GROUPS
-#define ZRC4_WIN_MAX_GROUPS 16   // aligned range batches of at most this many groups run 16 lanes per
-                                 // stream (crypt_win_kernel, zrc4_win.hpp); 0 = never
+#define ZRC4_WIN_MAX_GROUPS 16   // aligned range and grouped batches of at most this many groups run
+                                 // 16 lanes per stream (crypt_win_kernel, zrc4_win.hpp); 0 = never
 #endif
 
 struct zrc4_ctx {
@@ -98,9 +98,14 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
     const bool stream_kernel = mode != zrc4::kGrouped && grid > (uint32_t)c->num_cus;
     // Few aligned groups: 16 lanes per stream (speculative windows), one wave
     // per 4 streams, 64 workgroups per group.
-    if (!fr && mode == zrc4::kRange && (first_slot & 255u) == 0u && grid <= (uint32_t)ZRC4_WIN_MAX_GROUPS) {
-        hipLaunchKernelGGL(zrc4::crypt_win_kernel, dim3(64u * grid), dim3(64), 0, s, c->arena, c->xy, first_slot,
-                           payload, off, len, n);
+    if (!fr && grid <= (uint32_t)ZRC4_WIN_MAX_GROUPS &&
+        ((mode == zrc4::kRange && (first_slot & 255u) == 0u) || mode == zrc4::kGrouped)) {
+        if (mode == zrc4::kRange)
+            hipLaunchKernelGGL(zrc4::crypt_win_kernel<zrc4::kRange>, dim3(64u * grid), dim3(64), 0, s, c->arena,
+                               c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err);
+        else
+            hipLaunchKernelGGL(zrc4::crypt_win_kernel<zrc4::kGrouped>, dim3(64u * grid), dim3(64), 0, s, c->arena,
+                               c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err);
         return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
     }
     // Few whole groups: half-group workgroups, one per CU (2 waves per CU).

@@ -31,7 +31,7 @@
 // Arena access: the 4 streams of a workgroup are the 4 slots whose S-box
 // bytes share one dword of every image row (col bits 0-1 = lane >> 5,
 // wave & 1, see col_of), so the state moves as 256 aligned dword loads and
-// stores per workgroup: slots g*256 + 128h + L + 32b, b = 0..3, for dword
+// stores per workgroup: group-lanes 128h + L + 32b, b = 0..3, for dword
 // column q = 32h + L.
 #pragma once
 #include "zrc4_kernels.hpp"
@@ -181,33 +181,112 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
           "s42", "s43", "s44", "s45", "s46", "s47");
 }
 
-// Range batches with first_slot % 256 == 0 and few groups: grid = 64 x groups
-// workgroups of one wave.  Workgroup k -> (group, dword column) with the 8
+// Chain-bound launches with few groups: grid = 64 x groups (range batches
+// with first_slot % 256 == 0) or 64 x buckets (grouped batches) workgroups of
+// one wave.  Workgroup k -> (group or bucket, dword column) with the 8
 // columns of one XCD (k mod 8) adjacent, so a row's image bytes are shared by
 // few L2s.
+//   kRange:   stream b of dword column q is entry g*256 + 128h + L + 32b.
+//   kGrouped: every workgroup reads its bucket's 256 entries, checks the
+//             bucket contract as crypt_kernel<kGrouped> does (one group, no
+//             slot twice; else kErrGroup and the bucket is skipped whole) and
+//             builds slot -> entry, length, offset tables in LDS (in the ring,
+//             before the ring is used); the image load is issued from the
+//             first busy id's group ahead of the table build.
+template <int MODE>
 __global__ void __launch_bounds__(64)
-crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uint32_t first_slot,
-                 uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
-                 const uint32_t *__restrict__ len, uint32_t n)
+crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const uint32_t *__restrict__ ids,
+                 uint32_t first_slot, uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
+                 const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity, uint32_t *__restrict__ err)
 {
     __shared__ __attribute__((aligned(1024))) uint32_t Mk[kWinStreams * 256];
     __shared__ __attribute__((aligned(kWinRing))) uint8_t Ring[kWinStreams * kWinRing];
     __shared__ __attribute__((aligned(512))) uint8_t Sb[kWinStreams * 512];
 
     const uint32_t k = blockIdx.x, xcd = k & 7u, idx = k >> 3;
-    const uint32_t q = (idx & 7u) | (xcd << 3), g = idx >> 3;
+    const uint32_t q = (idx & 7u) | (xcd << 3), wg = idx >> 3;   // group (kRange) or bucket (kGrouped)
     const uint32_t lane = threadIdx.x, l = lane & 15u, b = lane >> 4;
-    const uint32_t e = g * kGroup + ((q >> 5) << 7) + (q & 31u) + 32u * b;   // entry of this lane's stream
-    const uint32_t slot = first_slot + e;
-    const bool valid = e < n;
-    if (!__builtin_amdgcn_ballot_w64(valid)) return;                          // whole dword column idle
-
-    uint8_t *img = arena + (size_t)(slot >> 8) * kGroupBytes + 4u * q;      // + row * 256
+    const uint32_t kb = ((q >> 5) << 7) + (q & 31u) + 32u * b;             // group-lane of this lane's stream
+    uint32_t slot, L = 0;
+    uint64_t O = 0;
+    bool valid;
     uint32_t rows[4];
+    if constexpr (MODE == kRange) {
+        const uint32_t e = wg * kGroup + kb;
+        slot = first_slot + e;
+        valid = e < n;
+        if (!__builtin_amdgcn_ballot_w64(valid)) return;                      // whole dword column idle
+        const uint8_t *img = arena + (size_t)(slot >> 8) * kGroupBytes + 4u * q;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
-    const uint32_t L = valid ? len[e] : 0u;
-    const uint64_t O = valid ? off[e] : 0u;
+        for (int r = 0; r < 4; ++r)
+            rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
+        if (valid) {
+            L = len[e];
+            O = off[e];
+        }
+    } else {
+        uint32_t *te = reinterpret_cast<uint32_t *>(Ring);                    // slot & 255 -> entry
+        uint32_t *tl = te + 256;                                              // length
+        uint64_t *to = reinterpret_cast<uint64_t *>(Ring + 2048);             // offset
+        uint32_t *fl = reinterpret_cast<uint32_t *>(Ring + 4096);             // 256-bit seen map, bad flag
+        uint32_t idq[4], lq[4];
+        uint64_t oq[4];
+        bool bq[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t e = wg * kGroup + lane + 64u * r;
+            const bool v = e < n;
+            uint32_t id = v ? ids[e] : ZRC4_INVALID;
+            lq[r] = v ? len[e] : 0u;
+            oq[r] = v ? off[e] : 0u;
+            if (v && id >= capacity && id != ZRC4_INVALID) {                 // ZRC4_IDLE_SLOT pads buckets
+                latch_fault(err, kErrSlotRange);
+                id = ZRC4_INVALID;
+            }
+            idq[r] = id;
+            bq[r] = id != ZRC4_INVALID && lq[r] != 0u;
+            te[lane + 64u * r] = ZRC4_INVALID;
+        }
+        if (lane < 9) fl[lane] = 0u;
+        uint32_t gw = ZRC4_INVALID;
+#pragma unroll
+        for (int r = 3; r >= 0; --r) {
+            const uint64_t bm = __builtin_amdgcn_ballot_w64(bq[r]);
+            if (bm) gw = __builtin_amdgcn_readlane(idq[r], (int)__builtin_ctzll(bm)) >> 8;
+        }
+        if (gw == ZRC4_INVALID) return;                                       // idle bucket
+        gw = __builtin_amdgcn_readfirstlane(gw);
+        const uint8_t *img = arena + (size_t)gw * kGroupBytes + 4u * q;      // speculative: the first busy id's group
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (bq[r]) {
+                const uint32_t kk = idq[r] & 255u;
+                if ((idq[r] >> 8) != gw) fl[8] = 1u;                                     // another group
+                if (atomicOr(&fl[kk >> 5], 1u << (kk & 31u)) & (1u << (kk & 31u))) fl[8] = 1u;   // a slot twice
+                te[kk] = wg * kGroup + lane + 64u * r;
+                tl[kk] = lq[r];
+                to[kk] = oq[r];
+            }
+        }
+        __syncthreads();
+        if (fl[8]) {
+            if (lane == 0) latch_fault(err, kErrGroup);
+            return;
+        }
+        slot = gw * 256u + kb;
+        valid = te[kb] != ZRC4_INVALID;
+        if (valid) {
+            L = tl[kb];
+            O = to[kb];
+        }
+        if (!__builtin_amdgcn_ballot_w64(valid)) return;
+        __syncthreads();                                                      // tables read before the ring is used
+    }
+    uint8_t *img = arena + (size_t)(slot >> 8) * kGroupBytes + 4u * q;
     const uint32_t sxy = valid ? xy[slot] : 0u;
     uint8_t *msg = payload + O;
     const bool aligned = ((uintptr_t)msg & 15u) == 0u;
@@ -244,8 +323,10 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uint32_
         const uint32_t c1 = L < c0 + kWinRing ? L : c0 + kWinRing;
         const uint32_t rem = c0 < L ? c1 - c0 : 0u;
         win_windows(w, rem, l, sb, mb, rb);
-        // XOR pass of [c0, c1): whole 16-byte units from the prefetch, bytes otherwise
-        if (aligned) {
+        // XOR pass of [c0, c1): whole 16-byte units from the prefetch, bytes
+        // otherwise (streams already past their end skip it: c1 - c0 would wrap)
+        if (c0 >= L) {
+        } else if (aligned) {
 #pragma unroll
             for (uint32_t u = 0; u < kWinUnits; ++u) {
                 const uint32_t pos = c0 + 16u * (l + kWinLanes * u);
@@ -256,8 +337,8 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uint32_
                     *reinterpret_cast<uint4 *>(msg + pos) = v;
                 }
             }
-            for (uint32_t pos = c0 + ((c1 - c0) & ~15u) + l; pos < c1; pos += kWinLanes)   // ragged tail
-                msg[pos] ^= R[pos & (kWinRing - 1u)];
+            const uint32_t tpos = c0 + ((c1 - c0) & ~15u) + l;                  // ragged tail: < 16 bytes
+            if (tpos < c1) msg[tpos] ^= R[tpos & (kWinRing - 1u)];
         } else {
             for (uint32_t pos = c0 + l; pos < c1; pos += kWinLanes) msg[pos] ^= R[pos & (kWinRing - 1u)];
         }
