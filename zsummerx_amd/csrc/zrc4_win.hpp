@@ -183,9 +183,7 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
 
 // Chain-bound launches with few groups: grid = 64 x groups (range batches
 // with first_slot % 256 == 0) or 64 x buckets (grouped batches) workgroups of
-// one wave.  Workgroup k -> (group or bucket, dword column) with the 8
-// columns of one XCD (k mod 8) adjacent, so a row's image bytes are shared by
-// few L2s.
+// one wave.
 //   kRange:   stream b of dword column q is entry g*256 + 128h + L + 32b.
 //   kGrouped: every workgroup reads its bucket's 256 entries, checks the
 //             bucket contract as crypt_kernel<kGrouped> does (one group, no
@@ -203,8 +201,13 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
     __shared__ __attribute__((aligned(kWinRing))) uint8_t Ring[kWinStreams * kWinRing];
     __shared__ __attribute__((aligned(512))) uint8_t Sb[kWinStreams * 512];
 
+    // workgroup k runs on XCD k mod 8.  With a multiple of 8 groups, all 64
+    // columns of a group sit on one XCD (its image lines fill one L2);
+    // otherwise the 8 columns an XCD takes from each group are adjacent.
     const uint32_t k = blockIdx.x, xcd = k & 7u, idx = k >> 3;
-    const uint32_t q = (idx & 7u) | (xcd << 3), wg = idx >> 3;   // group (kRange) or bucket (kGrouped)
+    const bool local = ((gridDim.x >> 6) & 7u) == 0u;
+    const uint32_t q = local ? (idx & 63u) : ((idx & 7u) | (xcd << 3));
+    const uint32_t wg = local ? (((idx >> 6) << 3) | xcd) : (idx >> 3);   // group (kRange) or bucket (kGrouped)
     const uint32_t lane = threadIdx.x, l = lane & 15u, b = lane >> 4;
     const uint32_t kb = ((q >> 5) << 7) + (q & 31u) + 32u * b;             // group-lane of this lane's stream
     uint32_t slot, L = 0;
