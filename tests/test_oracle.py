@@ -121,3 +121,31 @@ def test_synth_shard_consistency():
     assert np.array_equal(whole.keys.reshape(64, 16)[24:40], part.keys.reshape(16, 16))
     assert np.array_equal(whole.payload[24 * 256:40 * 256], part.payload)
     assert np.array_equal(whole.adv[24:40], part.adv)
+
+
+def test_window_rules_match_serial_prga():
+    """The speculative-window rules crypt_win_kernel runs (tools/window_sim.py,
+    DESIGN.md §3.8) reproduce the serial PRGA byte for byte and state for
+    state, from fresh and resumed streams, at the window widths 8 and 16; and
+    the committed prefix is never empty."""
+    import random
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+    import window_sim as ws
+    rng = random.Random(7)
+    for w in (8, 16):
+        for _ in range(6):
+            key = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 33)))
+            S = ws.ksa(key)
+            _, S, x, y = ws.prga_serial(S, 0, 0, rng.randrange(0, 400))
+            n = 700
+            want, Sw, xw, yw = ws.prga_serial(S, x, y, n)
+            got, Sg, xg, yg, windows = ws.prga_window(S, x, y, n, w)
+            assert got == want and (Sg, xg, yg) == (Sw, xw, yw)
+            assert windows <= n
+        # oracle agreement on the same key
+        r = pyoracle.Rc4(b"window")
+        S = ws.ksa(b"window")
+        got, *_ = ws.prga_window(S, 0, 0, 300, w)
+        assert bytes(got) == r.encryption(bytes(300))
