@@ -98,14 +98,22 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
     const bool stream_kernel = mode != zrc4::kGrouped && grid > (uint32_t)c->num_cus;
     // Few aligned groups: 16 lanes per stream (speculative windows), one wave
     // per 4 streams, 64 workgroups per group.
-    if (!fr && grid <= (uint32_t)ZRC4_WIN_MAX_GROUPS &&
+    if (grid <= (uint32_t)ZRC4_WIN_MAX_GROUPS &&
         ((mode == zrc4::kRange && (first_slot & 255u) == 0u) || mode == zrc4::kGrouped)) {
-        if (mode == zrc4::kRange)
-            hipLaunchKernelGGL(zrc4::crypt_win_kernel<zrc4::kRange>, dim3(64u * grid), dim3(64), 0, s, c->arena,
-                               c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err);
+        const dim3 wgrid(64u * grid), wblk(64);
+        const zrc4::FrameArgs fa = fr ? *fr : zrc4::FrameArgs{};
+        if (mode == zrc4::kRange && fr)
+            hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kRange, true>), wgrid, wblk, 0, s, c->arena, c->xy, ids,
+                               first_slot, payload, off, len, n, c->capacity, c->err, fa);
+        else if (mode == zrc4::kRange)
+            hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kRange, false>), wgrid, wblk, 0, s, c->arena, c->xy, ids,
+                               first_slot, payload, off, len, n, c->capacity, c->err, fa);
+        else if (fr)
+            hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kGrouped, true>), wgrid, wblk, 0, s, c->arena, c->xy,
+                               ids, first_slot, payload, off, len, n, c->capacity, c->err, fa);
         else
-            hipLaunchKernelGGL(zrc4::crypt_win_kernel<zrc4::kGrouped>, dim3(64u * grid), dim3(64), 0, s, c->arena,
-                               c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err);
+            hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kGrouped, false>), wgrid, wblk, 0, s, c->arena, c->xy,
+                               ids, first_slot, payload, off, len, n, c->capacity, c->err, fa);
         return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
     }
     // Few whole groups: half-group workgroups, one per CU (2 waves per CU).

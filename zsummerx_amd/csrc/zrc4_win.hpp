@@ -191,11 +191,17 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
 //             builds slot -> entry, length, offset tables in LDS (in the ring,
 //             before the ring is used); the image load is issued from the
 //             first busy id's group ahead of the table build.
-template <int MODE>
+//   FRAME:    onRecv's framing walk (frame_walk, §8f row 4) of every entry in
+//             the same launch: a stream's entry by its lane 0 once the
+//             stream's bytes are decrypted; grouped entries that decrypt
+//             nothing (idle ids, length 0, idle buckets) by lane q of the
+//             bucket's workgroup q (entries q + 64r), on the raw bytes.
+template <int MODE, bool FRAME>
 __global__ void __launch_bounds__(64)
 crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const uint32_t *__restrict__ ids,
                  uint32_t first_slot, uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
-                 const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity, uint32_t *__restrict__ err)
+                 const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity, uint32_t *__restrict__ err,
+                 FrameArgs fr)
 {
     __shared__ __attribute__((aligned(1024))) uint32_t Mk[kWinStreams * 256];
     __shared__ __attribute__((aligned(kWinRing))) uint8_t Ring[kWinStreams * kWinRing];
@@ -210,12 +216,13 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
     const uint32_t wg = local ? (((idx >> 6) << 3) | xcd) : (idx >> 3);   // group (kRange) or bucket (kGrouped)
     const uint32_t lane = threadIdx.x, l = lane & 15u, b = lane >> 4;
     const uint32_t kb = ((q >> 5) << 7) + (q & 31u) + 32u * b;             // group-lane of this lane's stream
-    uint32_t slot, L = 0;
+    uint32_t slot, L = 0, ent = 0;                                         // ent: this stream's batch entry
     uint64_t O = 0;
     bool valid;
     uint32_t rows[4];
     if constexpr (MODE == kRange) {
         const uint32_t e = wg * kGroup + kb;
+        ent = e;
         slot = first_slot + e;
         valid = e < n;
         if (!__builtin_amdgcn_ballot_w64(valid)) return;                      // whole dword column idle
@@ -257,6 +264,15 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             const uint64_t bm = __builtin_amdgcn_ballot_w64(bq[r]);
             if (bm) gw = __builtin_amdgcn_readlane(idq[r], (int)__builtin_ctzll(bm)) >> 8;
         }
+        if constexpr (FRAME) {                        // entries that decrypt nothing: raw framing
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t e = wg * kGroup + lane + 64u * r;
+                if (lane == q && e < n && !bq[r])
+                    frame_walk(payload + fr.off[e], fr.len[e], fr.bound, fr.maxp, e, fr.npk, fr.used, fr.status,
+                               fr.pkt_len);
+            }
+        }
         if (gw == ZRC4_INVALID) return;                                       // idle bucket
         gw = __builtin_amdgcn_readfirstlane(gw);
         const uint8_t *img = arena + (size_t)gw * kGroupBytes + 4u * q;      // speculative: the first busy id's group
@@ -281,7 +297,8 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             return;
         }
         slot = gw * 256u + kb;
-        valid = te[kb] != ZRC4_INVALID;
+        ent = te[kb];
+        valid = ent != ZRC4_INVALID;
         if (valid) {
             L = tl[kb];
             O = to[kb];
@@ -355,6 +372,14 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
     }
 
     if (valid && l == 0) xy[slot] = (uint16_t)(((w.xa - 1u) & 0xFFu) | ((w.y & 0xFFu) << 8));
+    if constexpr (FRAME) {
+        // the stream's 16 lanes stored its bytes: they must have landed
+        // before lane 0 reads the headers back
+        __builtin_amdgcn_s_waitcnt(0);
+        if (valid && l == 0)
+            frame_walk(payload + fr.off[ent], fr.len[ent], fr.bound, fr.maxp, ent, fr.npk, fr.used, fr.status,
+                       fr.pkt_len);
+    }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
