@@ -316,8 +316,11 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
                      "kernel_min_segment_us": round(min(kern_ms) * 1e3, 3),
                      "kernel_timing": f"HIP events bracketing {len(kern_ms)} segments of "
                                       f"{args.event_every} back-to-back timed launches (per-launch average)"},
-        "latency_ceiling_gibs": {"note": "chain-bound payload rate min(S,131072 resident)*2.4GHz/L_cyc",
-                                 "L70": round(latency_ceiling(S, L, 70), 1),
+        "latency_ceiling_gibs": {"note": "chain-bound payload rate min(S,131072 resident)*2.4GHz/L_cyc per "
+                                         "stream: L46 = 16 lanes per stream (crypt_win_kernel, <= 16 groups), "
+                                         "L96 = one lane per stream, L130 = one lane at 8 waves/CU",
+                                 "L46": round(latency_ceiling(S, L, 46), 1),
+                                 "L96": round(latency_ceiling(S, L, 96), 1),
                                  "L130": round(latency_ceiling(S, L, 130), 1)},
     }
 
