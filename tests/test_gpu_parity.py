@@ -670,3 +670,41 @@ def test_reservoir_round_trip(built, torch_cuda, where):
         c.sync()
         got = pay.cpu().numpy().reshape(S, total)
     assert np.array_equal(got, want)
+
+
+def test_window_tag_restart(built, torch_cuda):
+    """The window kernel's marker tags (24 bits) restart, with the markers
+    cleared, long before they could wrap.  A build that restarts them at
+    every chunk (ZRC4_WIN_TAG_LIMIT=4) stays bit-exact over multi-chunk
+    messages, range and grouped."""
+    from zsummerx_amd import build
+    torch = torch_cuda
+    var = build.build_variant("wintag4", build.TEST_VARIANTS["wintag4"])
+    rng = np.random.default_rng(77)
+    n = 600
+    keys = rng.integers(0, 256, 16 * n, dtype=np.uint8)
+    koff = np.arange(n, dtype=np.uint64) * 16
+    klen = np.full(n, 16, dtype=np.uint32)
+    ob = pyoracle.Batch(n)
+    ob.make_sbox(keys, koff, klen)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    s = torch.cuda.current_stream()
+    with Context(0, 1024, lib=var) as c:
+        c.ksa_range(0, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
+        for call in range(2):
+            L = rng.integers(2000, 9000, n).astype(np.uint32)
+            off = (np.concatenate([[0], np.cumsum((L.astype(np.uint64) + 15) // 16 * 16)[:-1]])).astype(np.uint64)
+            data = rng.integers(0, 256, int(off[-1] + L[-1]) + 16, dtype=np.uint8)
+            want = data.copy()
+            ob.crypt(want, off, L, threads=8)
+            pay = T(data)
+            if call == 0:
+                c.crypt_range(0, pay, T(off.view(np.int64)), T(L.view(np.int32)), stream=s)
+            else:
+                ids = np.arange(n, dtype=np.uint32)
+                got = data.copy()
+                c.crypt_host(got, off, L, ids=ids)
+                pay = T(got)
+            c.sync(s)
+            bad = np.flatnonzero(pay.cpu().numpy() != want)
+            assert bad.size == 0, (call, bad[:8], int(bad.size))

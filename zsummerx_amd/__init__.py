@@ -50,10 +50,12 @@ def _stream(s) -> C.c_void_p | None:
 
 
 class Context:
-    """One device, one arena of `capacity` RC4 streams (slots)."""
+    """One device, one arena of `capacity` RC4 streams (slots).  `lib`: an
+    A/B build of the same C-ABI (zsummerx_amd.build.build_variant), default the
+    product libzrc4.so."""
 
-    def __init__(self, device: int = 0, capacity: int = GROUP_SLOTS):
-        self._lib = load()
+    def __init__(self, device: int = 0, capacity: int = GROUP_SLOTS, lib=None):
+        self._lib = load(lib) if lib is not None else load()
         h = C.c_void_p()
         check(self._lib.zrc4_create(C.byref(h), int(device), int(capacity)), "zrc4_create")
         self._h = h

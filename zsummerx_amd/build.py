@@ -204,8 +204,15 @@ def build_oracle() -> None:
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
 
 
+# A/B builds the GPU tests load (tests/test_gpu_parity.py): built with the
+# product so that no test compiles on the GPU box.
+TEST_VARIANTS = {"wintag4": {"ZRC4_WIN_TAG_LIMIT": 4}}
+
+
 def build_all(force: bool = False) -> None:
     build_lib(force)
+    for name, defs in TEST_VARIANTS.items():
+        build_variant(name, defs)
     build_synth(force)
     build_frame(force)
     build_oracle()

@@ -42,6 +42,10 @@ constexpr uint32_t kWinLanes = 16;           // W: lanes (steps) per stream wind
 constexpr uint32_t kWinStreams = 4;          // streams per wave / workgroup
 constexpr uint32_t kWinRing = 2048;          // keystream chunk per stream (bytes)
 constexpr uint32_t kWinUnits = kWinRing / 16 / kWinLanes;   // 16-byte payload units per lane per chunk
+#ifndef ZRC4_WIN_TAG_LIMIT
+#define ZRC4_WIN_TAG_LIMIT (1u << 23)
+#endif
+constexpr uint32_t kWinTagLimit = ZRC4_WIN_TAG_LIMIT;      // marker tags restart past this (24-bit field)
 
 struct WinLane {
     uint32_t xa;     // x + 1 (byte)
@@ -342,6 +346,13 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
     for (uint32_t c0 = 0; __builtin_amdgcn_ballot_w64(c0 < L); c0 += kWinRing) {
         const uint32_t c1 = L < c0 + kWinRing ? L : c0 + kWinRing;
         const uint32_t rem = c0 < L ? c1 - c0 : 0u;
+        // window tags are 24 bits: long before they wrap (a 2 KiB chunk takes
+        // < 2 048 windows), the markers are cleared and the tags restart
+        if (w.v >= (kWinTagLimit << 8)) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) reinterpret_cast<uint4 *>(Mk)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+            w.v = (1u << 8) | (255u - l);
+        }
         win_windows(w, rem, l, sb, mb, rb);
         // XOR pass of [c0, c1): whole 16-byte units from the prefetch, bytes
         // otherwise (streams already past their end skip it: c1 - c0 would wrap)
