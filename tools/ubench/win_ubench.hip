@@ -394,7 +394,8 @@ win4_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint
 
 
 // v6: the product loop (zrc4::win_windows, zsummerx_amd/csrc/zrc4_win.hpp)
-// on a linear S-box layout: the tuning harness for the library kernel.
+// on a linear S-box layout: the tuning harness for the library kernel (the
+// loop uses only the first 256 bytes of each stream's 512-byte S area).
 __global__ void __launch_bounds__(64)
 win6_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
             uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)

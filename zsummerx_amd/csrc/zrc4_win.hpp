@@ -21,8 +21,9 @@
 // t_l = a_l + b_l, else S0[t_l].  About 10 bytes commit per window.
 //
 // One 64-thread workgroup = one wave = 4 streams x 16 lanes.  Per stream in
-// LDS: the S-box twice (bytes p and p + 256 always written together, so
-// S[x + 1 + l] and S[a + b] need no wrap), a 256-entry marker table
+// LDS: the S-box (256-aligned, so S[(x + 1 + l) mod 256] and S[(a + b) mod
+// 256] are one SDWA byte add into a register holding the base), a 256-entry
+// marker table
 // (ds_max of (window tag << 8) | (255 - l): the read-back names the lowest lane
 // whose j hit that byte this window -> the duplicate-j rule and the keystream
 // rule), and a keystream ring of kWinRing bytes.  Payload is XORed from the
@@ -69,8 +70,8 @@ struct WinLane {
 //   3. the duplicate-j rule, DPP OR over the 16 lanes with the keystream
 //      address work and S0[t] read in the DPP wait slots, cut = lowest bit
 //      (<= rem), x and window n+1's a_l address;
-//   4. commit (4 byte writes, both S copies) under exec = lanes < cut, window
-//      n+1's a_l read, S_final[t] and marker(t) reads, updates.
+//   4. commit (2 byte writes) under exec = lanes < cut, window n+1's a_l
+//      read, S_final[t] and marker(t) reads, updates.
 // Every DPP read of a VGPR sits at least two VALU ops (or an s_nop) after the
 // VALU write of it.  Pinned temporaries v106-v131, s[40:47].
 // (v_dot4_u32_u8 prefix sums over the window bytes were tried: the dot4
@@ -83,7 +84,7 @@ struct WinLane {
     "v_max_u32_dpp v120, v120, v120 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"           \
     "v_cmp_ge_u32_e64 s[42:43], v123, %[v]\n\t"                                                   \
     SCAN("row_shr:1")                                                                             \
-    "v_xor_b32 v127, 0x100, v106\n\t"                                                             \
+    "s_nop 0\n\t"                                                                                 \
     "v_max_u32_dpp v120, v120, v120 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"           \
     "s_or_b64 s[42:43], s[42:43], s[44:45]\n\t"                                                   \
     "v_cndmask_b32_e64 v124, v121, v122, s[42:43]\n\t"                                            \
@@ -101,7 +102,9 @@ struct WinLane {
     SCAN("row_shr:8")
 #define ZW_SCAN(CTRL) "v_add_u32_dpp v112, v112, v112 " CTRL " row_mask:0xf bank_mask:0xf\n\t"
 #define ZW_NOSCAN(CTRL) "s_nop 0\n\t"
-#define ZW_ADDR(XA) "v_add3_u32 v106, %[sb], " XA ", %[l]\n\t"
+#define ZW_ADDR(XA)                                                                               \
+    "v_add_u32_sdwa v106, " XA ", %[l] dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "  \
+    "src1_sel:DWORD\n\t"
 __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l, uint32_t sb, uint32_t mb,
                                             uint32_t rb)
 {
@@ -111,6 +114,8 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_and_b32 v120, 0xff, %[y]\n\t"
         "s_mov_b64 s[44:45], 0\n\t"
         "v_mov_b32 v123, 0\n\t"
+        "v_mov_b32 v106, %[sb]\n\t"                              // S base (256-aligned) in bytes 1-3
+        "v_mov_b32 v126, %[sb]\n\t"
         ZW_ADDR("%[xa]")
         "ds_read_u8 v107, v106\n\t"                             // a_l of window 0
         "ZW_LOOP_%=:\n\t"
@@ -138,7 +143,7 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_cmp_ne_u32 vcc, v117, %[v]\n\t"
         "v_cndmask_b32 v119, 0, %[bitl], vcc\n\t"
         "v_or_b32 v118, v118, v119\n\t"
-        "v_add3_u32 v126, %[sb], v107, v116\n\t"                // &S[a + b]: the doubled S wraps for free
+        "v_add_u32_sdwa v126, v107, v116 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t"   // &S[t]
         "v_add_u32 v128, v107, v116\n\t"
         "ds_read_u8 v121, v126\n\t"                             // S0[t]
         "v_or_b32_dpp v118, v118, v118 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
@@ -160,10 +165,8 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         // 4. commit, then window n+1's read right behind it
         "s_and_saveexec_b64 s[40:41], vcc\n\t"
         "s_mov_b64 s[46:47], exec\n\t"
-        "ds_write_b8 v131, v116\n\t"                            // S[i_l] = b_l, both copies
-        "ds_write_b8 v127, v116\n\t"
-        "ds_write_b8 v114, v107\n\t"                            // S[J_l] = a_l, both copies
-        "ds_write_b8 v114, v107 offset:256\n\t"
+        "ds_write_b8 v131, v116\n\t"                            // S[i_l] = b_l
+        "ds_write_b8 v114, v107\n\t"                            // S[J_l] = a_l
         "s_mov_b64 exec, s[40:41]\n\t"
         "v_cndmask_b32 v120, %[y], v130, vcc\n\t"
         "ds_read_u8 v107, v106\n\t"                             // a_l of window n+1
@@ -181,7 +184,7 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         : [l] "v"(l), [sb] "v"(sb), [mb] "v"(mb), [rb] "v"(rb), [bitl] "v"(bitl), [l1] "v"(l1),
           [rmask] "s"(kWinRing - 1)
         : "memory", "vcc", "scc", "v106", "v107", "v112", "v114", "v115", "v116", "v117", "v118", "v119", "v120",
-          "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "s40", "s41",
+          "v121", "v122", "v123", "v124", "v125", "v126", "v128", "v129", "v130", "v131", "s40", "s41",
           "s42", "s43", "s44", "s45", "s46", "s47");
 }
 
@@ -209,7 +212,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
 {
     __shared__ __attribute__((aligned(1024))) uint32_t Mk[kWinStreams * 256];
     __shared__ __attribute__((aligned(kWinRing))) uint8_t Ring[kWinStreams * kWinRing];
-    __shared__ __attribute__((aligned(512))) uint8_t Sb[kWinStreams * 512];
+    __shared__ __attribute__((aligned(256))) uint8_t Sb[kWinStreams * 256];
 
     // workgroup k runs on XCD k mod 8.  With a multiple of 8 groups, all 64
     // columns of a group sit on one XCD (its image lines fill one L2);
@@ -323,7 +326,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
         if (aligned && pos + 16u <= L) pre[u] = *reinterpret_cast<const uint4 *>(msg + pos);
     }
 
-    uint8_t *S = Sb + b * 512u;
+    uint8_t *S = Sb + b * 256u;
     uint32_t *M = Mk + b * 256u;
     uint8_t *R = Ring + b * kWinRing;
 #pragma unroll
@@ -332,8 +335,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
 #pragma unroll
         for (uint32_t s4 = 0; s4 < 4; ++s4) {
             const uint8_t v = (uint8_t)(rows[r] >> (8 * s4));
-            Sb[s4 * 512u + kk] = v;
-            Sb[s4 * 512u + 256u + kk] = v;
+            Sb[s4 * 256u + kk] = v;
         }
     }
 #pragma unroll
@@ -395,8 +397,8 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const uint32_t kk = lane + 64u * r;
-        const uint32_t v = (uint32_t)Sb[kk] | ((uint32_t)Sb[512u + kk] << 8) | ((uint32_t)Sb[1024u + kk] << 16) |
-                           ((uint32_t)Sb[1536u + kk] << 24);
+        const uint32_t v = (uint32_t)Sb[kk] | ((uint32_t)Sb[256u + kk] << 8) | ((uint32_t)Sb[512u + kk] << 16) |
+                           ((uint32_t)Sb[768u + kk] << 24);
         *reinterpret_cast<uint32_t *>(img + (size_t)kk * 256u) = v;
     }
 }
