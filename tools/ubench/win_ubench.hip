@@ -13,6 +13,7 @@
 #include <random>
 #include <algorithm>
 #include "../../zsummerx_amd/csrc/zrc4_win.hpp"
+#include "win64_loop.hpp"
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 constexpr int MAXN = (int)zrc4::kWinRing;   // keystream ring per stream (bytes)
@@ -435,6 +436,50 @@ win6_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint
     }
 }
 
+// v7: one stream per wave, W = 64 (zrc4::win64_windows).
+__global__ void __launch_bounds__(64)
+win7_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+            uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    __shared__ __attribute__((aligned(1024))) uint32_t M[256];
+    __shared__ __attribute__((aligned(MAXN))) uint8_t R[MAXN];
+    __shared__ __attribute__((aligned(256))) uint8_t S[256];
+    const uint32_t l = threadIdx.x;
+    const int s = blockIdx.x;
+    for (int k = 0; k < 4; ++k) {
+        S[l * 4 + k] = sbox_in[(size_t)s * 256 + l * 4 + k];
+        M[l * 4 + k] = 0;
+    }
+    const uint32_t sxy = xy_in[s];
+    __syncthreads();
+    uint32_t xa = __builtin_amdgcn_readfirstlane(((sxy & 0xFFu) + 1u) & 0xFFu);
+    uint32_t y = __builtin_amdgcn_readfirstlane(sxy >> 8);
+    uint32_t rp = 0, v = (1u << 8) | (255u - l);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#ifdef ZW64_DEBUG_CAP
+    uint32_t dbg[4];
+    zrc4::win64_windows(xa, y, v, (uint32_t)N, rp, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
+                        (uint32_t)(uintptr_t)R, dbg);
+    if (s == 0 && l < 12) printf("lane %u J %u maxM %x maddr %x d %u\n", l, dbg[0], dbg[1], dbg[2], dbg[3]);
+#else
+    zrc4::win64_windows(xa, y, v, (uint32_t)N, rp, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
+                        (uint32_t)(uintptr_t)R);
+#endif
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    for (int k = 0; k < N / 64; ++k) ks_out[(size_t)s * N + l * (N / 64) + k] = R[l * (N / 64) + k];
+    for (int k = 0; k < 4; ++k) sbox_out[(size_t)s * 256 + l * 4 + k] = S[l * 4 + k];
+    if (l == 0) {
+        xy_out[s] = (uint16_t)(((xa - 1) & 255) | ((y & 255) << 8));
+        cyc[s] = t1 - t0;
+        wins[s] = (v >> 8) - 1;
+#ifdef ZW64_DEBUG_CAP
+        printf("dbg stream %d: rp(cut total) %u xa %u y %u v %x R %u %u %u %u %u %u S[188] %u M[188] %x M[76] %x M[235] %x\n", s, rp, xa, y, v,
+               R[0], R[1], R[2], R[3], R[4], R[5], S[188], M[188], M[76], M[235]);
+#endif
+    }
+}
+
 static void ksa(uint8_t *S, const uint8_t *key, int kl)
 {
     for (int i = 0; i < 256; ++i) S[i] = (uint8_t)i;
@@ -496,7 +541,8 @@ static void run(int ns, int N, int reps)
     std::vector<float> ms;
     for (int r = 0; r < reps; ++r) {
         CHECK(hipEventRecord(e0));
-        if (V3 == 6) win6_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        if constexpr (V3 == 7) win7_kernel<<<ns, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if (V3 == 6) win6_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if (V3 == 2) win4_kernel<WPB><<<blocks, 64 * WPB>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if (V3) win3_kernel<W, WPB><<<blocks, 64 * WPB>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else win_kernel<W, WPB><<<blocks, 64 * WPB>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
@@ -540,7 +586,8 @@ int main(int argc, char **argv)
     const int wpb = argc > 4 ? atoi(argv[4]) : 1;
     if (N > MAXN || N % 16) { printf("bytes must be a multiple of 16 and <= %d\n", MAXN); return 1; }
     const int v3 = argc > 5 ? atoi(argv[5]) : 1;
-    if (v3 == 6) run<16, 1, 6>(ns, N, 20);
+    if (v3 == 7) run<64, 1, 7>(ns, N, 20);
+    else if (v3 == 6) run<16, 1, 6>(ns, N, 20);
     else if (v3 == 2) { if (wpb == 1) run<16, 1, 2>(ns, N, 20); else run<16, 2, 2>(ns, N, 20); }
     else if (v3) { if (w == 8) run<8, 1, 1>(ns, N, 20); else if (wpb == 1) run<16, 1, 1>(ns, N, 20); else run<16, 2, 1>(ns, N, 20); }
     else if (w == 8) { if (wpb == 1) run<8, 1, 0>(ns, N, 20); else run<8, 2, 0>(ns, N, 20); }
