@@ -66,12 +66,16 @@ struct WinLane {
 //      (S_final if a committed step <= l wrote t, else S0) and ring store fill
 //      the DPP wait slots;
 //   2. b_l = S0[J_l] and the marker max / read-back issue; under that round
-//      trip the d rule (one-hot of med3(d, l, 16), none when d == l);
-//   3. the duplicate-j rule, DPP OR over the 16 lanes with the keystream
-//      address work and S0[t] read in the DPP wait slots, cut = lowest bit
-//      (<= rem), x and window n+1's a_l address;
+//      trip the d rule (one-hot of med3(d, l, 16), none when d == l), the
+//      rem cap (bit min(rem, 16)) and the same one-hot plus bit l for a
+//      duplicate j;
+//   3. the duplicate-j rule (a select), DPP OR over the 16 lanes with the
+//      keystream address work and S0[t] read in the DPP wait slots, cut =
+//      lowest bit, window n+1's a_l address = this one's plus cut (SDWA byte
+//      add into the base register);
 //   4. commit (2 byte writes) under exec = lanes < cut, window n+1's a_l
-//      read, S_final[t] and marker(t) reads, updates.
+//      read, S_final[t] and marker(t) reads, then x, rem, the ring position
+//      and the commit mask under that round trip.
 // Every DPP read of a VGPR sits at least two VALU ops (or an s_nop) after the
 // VALU write of it.  Pinned temporaries v106-v131, s[40:47].
 // (v_dot4_u32_u8 prefix sums over the window bytes were tried: the dot4
@@ -121,28 +125,31 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "ZW_LOOP_%=:\n\t"
         // 1. scan of a, tail of window n-1
         ZW_TAIL_SCAN(ZW_SCAN)
-        "v_and_b32 %[y], 0xff, v120\n\t"
-        "v_add_u32 v112, v112, %[y]\n\t"
-        // 2. b / marker round trip, d rule under it
+        "v_add_u32 v112, v112, v120\n\t"                       // + y' (byte 0 of v120; J is masked below)
+        // 2. b / marker round trip, d rule and rem cap under it
         "v_add_u32_sdwa v114, %[sb], v112 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"
         "v_and_b32 v112, 0xff, v112\n\t"                       // J
         "v_lshl_add_u32 v115, v112, 2, %[mb]\n\t"
         "ds_read_u8 v116, v114\n\t"                             // b_l = S0[J]
         "ds_max_u32 v115, %[v]\n\t"
         "ds_read_b32 v117, v115\n\t"                            // lowest lane with this J
+        "v_and_b32 %[y], 0xff, v120\n\t"
         "v_sub_u32 v118, v112, %[xa]\n\t"
         "v_and_b32 v118, 0xff, v118\n\t"                       // d
         "v_med3_u32 v119, v118, %[l], 16\n\t"
         "v_cmp_ne_u32 vcc, v118, %[l]\n\t"
         "v_cndmask_b32 v119, 16, v119, vcc\n\t"
         "v_lshlrev_b32 v118, v119, 1\n\t"                       // bit 16 = no d conflict
+        "v_min_u32 v119, 16, %[rem]\n\t"
+        "v_lshlrev_b32 v119, v119, 1\n\t"
+        "v_or_b32 v118, v118, v119\n\t"                        // + bit min(rem, 16): cut <= rem
+        "v_or_b32 v119, v118, %[bitl]\n\t"                     // the same if this lane's J repeats
         "v_or_b32 v130, %[l1], v112\n\t"                        // y' candidate of this lane
         "v_bfi_b32 v125, %[rmask], %[rp], %[rb]\n\t"            // ring slot of this lane
         "s_waitcnt lgkmcnt(0)\n\t"
         // 3. duplicate-J rule, OR over the stream's 16 lanes, cut
         "v_cmp_ne_u32 vcc, v117, %[v]\n\t"
-        "v_cndmask_b32 v119, 0, %[bitl], vcc\n\t"
-        "v_or_b32 v118, v118, v119\n\t"
+        "v_cndmask_b32 v118, v118, v119, vcc\n\t"
         "v_add_u32_sdwa v126, v107, v116 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD\n\t"   // &S[t]
         "v_add_u32 v128, v107, v116\n\t"
         "ds_read_u8 v121, v126\n\t"                             // S0[t]
@@ -156,22 +163,21 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_cmp_le_u32_e64 s[44:45], v131, %[l]\n\t"             // t is the i of a step <= l
         "v_mov_b32 v131, v106\n\t"                              // &S[i_l] of window n
         "v_or_b32_dpp v118, v118, v118 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "v_ffbl_b32 v118, v118\n\t"
-        "v_min_u32 v118, v118, %[rem]\n\t"                      // cut
-        "v_add_u32 %[xa], %[xa], v118\n\t"
-        "v_and_b32 %[xa], 0xff, %[xa]\n\t"
+        "v_ffbl_b32 v118, v118\n\t"                             // cut
         "v_cmp_lt_u32 vcc, %[l], v118\n\t"
-        ZW_ADDR("%[xa]")                                        // window n+1's a_l address
+        "v_add_u32_sdwa v106, v106, v118 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0 src1_sel:DWORD\n\t"   // window n+1's a_l address
         // 4. commit, then window n+1's read right behind it
         "s_and_saveexec_b64 s[40:41], vcc\n\t"
-        "s_mov_b64 s[46:47], exec\n\t"
         "ds_write_b8 v131, v116\n\t"                            // S[i_l] = b_l
         "ds_write_b8 v114, v107\n\t"                            // S[J_l] = a_l
         "s_mov_b64 exec, s[40:41]\n\t"
-        "v_cndmask_b32 v120, %[y], v130, vcc\n\t"
         "ds_read_u8 v107, v106\n\t"                             // a_l of window n+1
         "ds_read_u8 v122, v126\n\t"                             // S_final[t]
         "ds_read_b32 v123, v129\n\t"                            // lowest lane whose J == t
+        "s_and_b64 s[46:47], vcc, s[40:41]\n\t"                 // commit mask (ring store next iteration)
+        "v_cndmask_b32 v120, %[y], v130, vcc\n\t"
+        "v_add_u32 %[xa], %[xa], v118\n\t"
+        "v_and_b32 %[xa], 0xff, %[xa]\n\t"
         "v_sub_u32 %[rem], %[rem], v118\n\t"
         "v_add_u32 %[rp], %[rp], v118\n\t"
         "v_cmp_ne_u32 vcc, 0, %[rem]\n\t"
