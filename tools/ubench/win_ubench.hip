@@ -15,6 +15,7 @@
 #include "../../zsummerx_amd/csrc/zrc4_win.hpp"
 #include "win64_loop.hpp"
 #include "win12_loop.hpp"
+#include "win_var.hpp"
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 constexpr int MAXN = (int)zrc4::kWinRing;   // keystream ring per stream (bytes)
@@ -479,6 +480,174 @@ win8_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint
     }
 }
 
+// v9: variant A (tools/ubench/win_var.hpp) (zrc4::win_windows, zsummerx_amd/csrc/zrc4_win.hpp)
+// on a linear S-box layout: the tuning harness for the library kernel (the
+// loop uses only the first 256 bytes of each stream's 512-byte S area).
+__global__ void __launch_bounds__(64)
+win9_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+            uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int W = 16, SPW = 4;
+    __shared__ __attribute__((aligned(1024))) uint32_t Mk[SPW * 256];
+    __shared__ __attribute__((aligned(MAXN))) uint8_t Ring[SPW * MAXN];
+    __shared__ __attribute__((aligned(512))) uint8_t Sb[SPW * 512];
+    const uint32_t lane = threadIdx.x, l = lane % W, g = lane / W;
+    const int s = blockIdx.x * SPW + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 512;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        const uint8_t v = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        S[l * (256 / W) + k] = v;
+        S[256 + l * (256 / W) + k] = v;
+        M[l * (256 / W) + k] = 0;
+    }
+    const uint32_t sxy = live ? xy_in[s] : 0;
+    __syncthreads();
+    zrc4::WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    zrc4::win_windows_A(w, live ? (uint32_t)N : 0u, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
+                      (uint32_t)(uintptr_t)R);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((w.xa - 1) & 255) | ((w.y & 255) << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = (w.v >> 8) - 1;
+        }
+    }
+}
+
+// v10: same as v6 since v17 (variant B shipped) (zrc4::win_windows, zsummerx_amd/csrc/zrc4_win.hpp)
+// on a linear S-box layout: the tuning harness for the library kernel (the
+// loop uses only the first 256 bytes of each stream's 512-byte S area).
+__global__ void __launch_bounds__(64)
+win10_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+            uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int W = 16, SPW = 4;
+    __shared__ __attribute__((aligned(1024))) uint32_t Mk[SPW * 256];
+    __shared__ __attribute__((aligned(MAXN))) uint8_t Ring[SPW * MAXN];
+    __shared__ __attribute__((aligned(512))) uint8_t Sb[SPW * 512];
+    const uint32_t lane = threadIdx.x, l = lane % W, g = lane / W;
+    const int s = blockIdx.x * SPW + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 512;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        const uint8_t v = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        S[l * (256 / W) + k] = v;
+        S[256 + l * (256 / W) + k] = v;
+        M[l * (256 / W) + k] = 0;
+    }
+    const uint32_t sxy = live ? xy_in[s] : 0;
+    __syncthreads();
+    zrc4::WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    zrc4::win_windows(w, live ? (uint32_t)N : 0u, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
+                      (uint32_t)(uintptr_t)R);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((w.xa - 1) & 255) | ((w.y & 255) << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = (w.v >> 8) - 1;
+        }
+    }
+}
+
+// v10: variant C (tools/ubench/win_var.hpp) (zrc4::win_windows, zsummerx_amd/csrc/zrc4_win.hpp)
+// on a linear S-box layout: the tuning harness for the library kernel (the
+// loop uses only the first 256 bytes of each stream's 512-byte S area).
+__global__ void __launch_bounds__(64)
+win11_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+            uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int W = 16, SPW = 4;
+    __shared__ __attribute__((aligned(1024))) uint32_t Mk[SPW * 256];
+    __shared__ __attribute__((aligned(MAXN))) uint8_t Ring[SPW * MAXN];
+    __shared__ __attribute__((aligned(512))) uint8_t Sb[SPW * 512];
+    const uint32_t lane = threadIdx.x, l = lane % W, g = lane / W;
+    const int s = blockIdx.x * SPW + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 512;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        const uint8_t v = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        S[l * (256 / W) + k] = v;
+        S[256 + l * (256 / W) + k] = v;
+        M[l * (256 / W) + k] = 0;
+    }
+    const uint32_t sxy = live ? xy_in[s] : 0;
+    __syncthreads();
+    zrc4::WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    zrc4::win_windows_C(w, live ? (uint32_t)N : 0u, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
+                      (uint32_t)(uintptr_t)R);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((w.xa - 1) & 255) | ((w.y & 255) << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = (w.v >> 8) - 1;
+        }
+    }
+}
+
+// v10: variant D (tools/ubench/win_var.hpp) (zrc4::win_windows, zsummerx_amd/csrc/zrc4_win.hpp)
+// on a linear S-box layout: the tuning harness for the library kernel (the
+// loop uses only the first 256 bytes of each stream's 512-byte S area).
+__global__ void __launch_bounds__(64)
+win12_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+            uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int W = 16, SPW = 4;
+    __shared__ __attribute__((aligned(1024))) uint32_t Mk[SPW * 256];
+    __shared__ __attribute__((aligned(MAXN))) uint8_t Ring[SPW * MAXN];
+    __shared__ __attribute__((aligned(512))) uint8_t Sb[SPW * 512];
+    const uint32_t lane = threadIdx.x, l = lane % W, g = lane / W;
+    const int s = blockIdx.x * SPW + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 512;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        const uint8_t v = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        S[l * (256 / W) + k] = v;
+        S[256 + l * (256 / W) + k] = v;
+        M[l * (256 / W) + k] = 0;
+    }
+    const uint32_t sxy = live ? xy_in[s] : 0;
+    __syncthreads();
+    zrc4::WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    zrc4::win_windows_D(w, live ? (uint32_t)N : 0u, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
+                      (uint32_t)(uintptr_t)R);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((w.xa - 1) & 255) | ((w.y & 255) << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = (w.v >> 8) - 1;
+        }
+    }
+}
+
 // v7: one stream per wave, W = 64 (zrc4::win64_windows).
 __global__ void __launch_bounds__(64)
 win7_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
@@ -584,7 +753,11 @@ static void run(int ns, int N, int reps)
     std::vector<float> ms;
     for (int r = 0; r < reps; ++r) {
         CHECK(hipEventRecord(e0));
-        if constexpr (V3 == 8) win8_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        if constexpr (V3 == 12) win12_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if constexpr (V3 == 11) win11_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if constexpr (V3 == 10) win10_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if constexpr (V3 == 9) win9_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if constexpr (V3 == 8) win8_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if constexpr (V3 == 7) win7_kernel<<<ns, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if (V3 == 6) win6_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if (V3 == 2) win4_kernel<WPB><<<blocks, 64 * WPB>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
@@ -630,7 +803,11 @@ int main(int argc, char **argv)
     const int wpb = argc > 4 ? atoi(argv[4]) : 1;
     if (N > MAXN || N % 16) { printf("bytes must be a multiple of 16 and <= %d\n", MAXN); return 1; }
     const int v3 = argc > 5 ? atoi(argv[5]) : 1;
-    if (v3 == 8) run<16, 1, 8>(ns, N, 20);
+    if (v3 == 12) run<16, 1, 12>(ns, N, 20);
+    else if (v3 == 11) run<16, 1, 11>(ns, N, 20);
+    else if (v3 == 10) run<16, 1, 10>(ns, N, 20);
+    else if (v3 == 9) run<16, 1, 9>(ns, N, 20);
+    else if (v3 == 8) run<16, 1, 8>(ns, N, 20);
     else if (v3 == 7) run<64, 1, 7>(ns, N, 20);
     else if (v3 == 6) run<16, 1, 6>(ns, N, 20);
     else if (v3 == 2) { if (wpb == 1) run<16, 1, 2>(ns, N, 20); else run<16, 2, 2>(ns, N, 20); }

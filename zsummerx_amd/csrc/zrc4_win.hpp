@@ -59,14 +59,15 @@ struct WinLane {
 // lane, equal inside a stream's 16 lanes; 0 = idle).  One asm statement; the
 // loop is rotated so that window n+1's read leaves right behind window n's
 // commit writes.  Per iteration n (a_l of window n already in flight):
-//   1. two interleaved DPP chains: the inclusive scan of a over the stream's
-//      16 lanes (row_shr 1, 2, 4, 8: J_l = y + a_0 + .. + a_l) and window
-//      n-1's y' = J of its last committed lane (max over the 16 lanes of
-//      (l + 1) << 8 | J, else the old y); window n-1's keystream select
-//      (S_final if a committed step <= l wrote t, else S0) and ring store fill
-//      the DPP wait slots;
-//   2. b_l = S0[J_l] and the marker max / read-back issue; under that round
-//      trip the d rule (one-hot of med3(d, l, 16), none when d == l), the
+//   1. two DPP chains interleaved step for step, so neither needs an s_nop:
+//      the inclusive scan of a over the stream's 16 lanes (row_shr 1, 2, 4,
+//      8: J_l = y + a_0 + .. + a_l; step 1 reads the a_l load directly, zero
+//      at row starts) and window n-1's y' = J of its last committed lane (max
+//      over the 16 lanes of (l + 1) << 8 | J, else the old y); window n-1's
+//      keystream select (S_final if a committed step <= l wrote t, else S0)
+//      in the last slots;
+//   2. b_l = S0[J_l] and the marker max / read-back issue, window n-1's ring
+//      store behind them (not waited for); under that round trip the d rule (one-hot of med3(d, l, 16), none when d == l), the
 //      rem cap (bit min(rem, 16)) and the same one-hot plus bit l for a
 //      duplicate j;
 //   3. the duplicate-j rule (a select), DPP OR over the 16 lanes with the
@@ -82,30 +83,6 @@ struct WinLane {
 // accumulator chain read stale values on MI355X -- bit-exact only because the
 // wrong j always tripped the duplicate rule -- and the DPP scan needs no
 // window bytes at all.)
-#define ZW_TAIL_SCAN(SCAN)                                                                        \
-    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
-    "v_mov_b32 v112, v107\n\t"                                                                    \
-    "v_max_u32_dpp v120, v120, v120 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"           \
-    "v_cmp_ge_u32_e64 s[42:43], v123, %[v]\n\t"                                                   \
-    SCAN("row_shr:1")                                                                             \
-    "s_nop 0\n\t"                                                                                 \
-    "v_max_u32_dpp v120, v120, v120 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"           \
-    "s_or_b64 s[42:43], s[42:43], s[44:45]\n\t"                                                   \
-    "v_cndmask_b32_e64 v124, v121, v122, s[42:43]\n\t"                                            \
-    SCAN("row_shr:2")                                                                             \
-    "v_add_u32 %[v], 0x100, %[v]\n\t"                                                             \
-    "v_max_u32_dpp v120, v120, v120 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"               \
-    "s_mov_b64 s[40:41], exec\n\t"                                                                \
-    "s_nop 0\n\t"                                                                                 \
-    SCAN("row_shr:4")                                                                             \
-    "s_mov_b64 exec, s[46:47]\n\t"                                                                \
-    "ds_write_b8 v125, v124\n\t"                                                                  \
-    "s_mov_b64 exec, s[40:41]\n\t"                                                                \
-    "v_max_u32_dpp v120, v120, v120 row_mirror row_mask:0xf bank_mask:0xf\n\t"                    \
-    "s_nop 1\n\t"                                                                                 \
-    SCAN("row_shr:8")
-#define ZW_SCAN(CTRL) "v_add_u32_dpp v112, v112, v112 " CTRL " row_mask:0xf bank_mask:0xf\n\t"
-#define ZW_NOSCAN(CTRL) "s_nop 0\n\t"
 #define ZW_ADDR(XA)                                                                               \
     "v_add_u32_sdwa v106, " XA ", %[l] dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "  \
     "src1_sel:DWORD\n\t"
@@ -124,7 +101,19 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "ds_read_u8 v107, v106\n\t"                             // a_l of window 0
         "ZW_LOOP_%=:\n\t"
         // 1. scan of a, tail of window n-1
-        ZW_TAIL_SCAN(ZW_SCAN)
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_add_u32_dpp v112, v107, v107 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_max_u32_dpp v120, v120, v120 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_cmp_ge_u32_e64 s[42:43], v123, %[v]\n\t"
+        "v_add_u32_dpp v112, v112, v112 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_u32_dpp v120, v120, v120 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_add_u32 %[v], 0x100, %[v]\n\t"
+        "v_add_u32_dpp v112, v112, v112 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_u32_dpp v120, v120, v120 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_or_b64 s[42:43], s[42:43], s[44:45]\n\t"
+        "v_cndmask_b32_e64 v124, v121, v122, s[42:43]\n\t"
+        "v_add_u32_dpp v112, v112, v112 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_u32_dpp v120, v120, v120 row_mirror row_mask:0xf bank_mask:0xf\n\t"
         "v_add_u32 v112, v112, v120\n\t"                       // + y' (byte 0 of v120; J is masked below)
         // 2. b / marker round trip, d rule and rem cap under it
         "v_add_u32_sdwa v114, %[sb], v112 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"
@@ -133,6 +122,10 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "ds_read_u8 v116, v114\n\t"                             // b_l = S0[J]
         "ds_max_u32 v115, %[v]\n\t"
         "ds_read_b32 v117, v115\n\t"                            // lowest lane with this J
+        "s_mov_b64 s[40:41], exec\n\t"
+        "s_mov_b64 exec, s[46:47]\n\t"
+        "ds_write_b8 v125, v124\n\t"                            // window n-1's ring store, behind the round trip
+        "s_mov_b64 exec, s[40:41]\n\t"
         "v_and_b32 %[y], 0xff, v120\n\t"
         "v_sub_u32 v118, v112, %[xa]\n\t"
         "v_and_b32 v118, 0xff, v118\n\t"                       // d
@@ -146,7 +139,7 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_or_b32 v119, v118, %[bitl]\n\t"                     // the same if this lane's J repeats
         "v_or_b32 v130, %[l1], v112\n\t"                        // y' candidate of this lane
         "v_bfi_b32 v125, %[rmask], %[rp], %[rb]\n\t"            // ring slot of this lane
-        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_waitcnt lgkmcnt(1)\n\t"
         // 3. duplicate-J rule, OR over the stream's 16 lanes, cut
         "v_cmp_ne_u32 vcc, v117, %[v]\n\t"
         "v_cndmask_b32 v118, v118, v119, vcc\n\t"
@@ -183,7 +176,20 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_cmp_ne_u32 vcc, 0, %[rem]\n\t"
         "s_cbranch_vccnz ZW_LOOP_%=\n\t"
         // drain: tail of the last window (window n's read is harmless)
-        ZW_TAIL_SCAN(ZW_NOSCAN)
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_max_u32_dpp v120, v120, v120 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_cmp_ge_u32_e64 s[42:43], v123, %[v]\n\t"
+        "s_or_b64 s[42:43], s[42:43], s[44:45]\n\t"
+        "v_cndmask_b32_e64 v124, v121, v122, s[42:43]\n\t"
+        "v_max_u32_dpp v120, v120, v120 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp v120, v120, v120 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp v120, v120, v120 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_mov_b64 s[40:41], exec\n\t"
+        "s_mov_b64 exec, s[46:47]\n\t"
+        "ds_write_b8 v125, v124\n\t"
+        "s_mov_b64 exec, s[40:41]\n\t"
         "v_and_b32 %[y], 0xff, v120\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
         : [xa] "+v"(w.xa), [y] "+v"(w.y), [v] "+v"(w.v), [rem] "+v"(rem), [rp] "+v"(w.rp)
