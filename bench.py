@@ -325,7 +325,7 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
     }
 
 
-WIN_MAX_GROUPS = 16   # zrc4.hip ZRC4_WIN_MAX_GROUPS
+WIN_MAX_GROUPS = 32   # zrc4.hip ZRC4_WIN_MAX_GROUPS
 
 
 def kernel_name(S: int, ids: str = "range") -> str:

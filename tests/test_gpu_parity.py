@@ -386,10 +386,10 @@ def test_direct_path_block_edges(built, torch_cuda, first_slot):
             assert (sb, x, y) == (bytes(want_sb), wx, wy), i
 
 
-# ------------------------- speculative-window path (crypt_win_kernel, <= 16 groups)
-@pytest.mark.parametrize("first_slot,n", [(0, 16 * 256 - 37), (768, 5)])
+# ------------------------- speculative-window path (crypt_win_kernel, <= 32 groups)
+@pytest.mark.parametrize("first_slot,n", [(0, 16 * 256 - 37), (768, 5), (256, 32 * 256 - 100)])
 def test_window_path_ragged(built, torch_cuda, first_slot, n):
-    """Aligned range batches of at most 16 groups run 16 lanes per stream
+    """Aligned range batches of at most 32 groups run 16 lanes per stream
     (zsummerx_amd/csrc/zrc4_win.hpp).  Lengths 0..5000 including every
     16-byte edge and messages longer than the 2 KiB keystream chunk (2-3
     chunks), 16-byte aligned and unaligned message starts (the byte path),
@@ -453,12 +453,13 @@ def grouped_batch(rng, n_groups, groups_total, fill=(1, 256)):
 
 
 @pytest.mark.parametrize("fill,nb,trunc", [((256, 256), 64, 0), ((1, 256), 64, 0), ((1, 256), 200, 0),
-                                           ((1, 200), 64, 100), ((1, 256), 200, 37)])
+                                           ((1, 200), 64, 100), ((1, 256), 200, 37), ((1, 256), 27, 11)])
 def test_grouped_ids_bit_exact(built, torch_cuda, fill, nb, trunc):
     """zrc4_crypt_grouped: each bucket a subset of ONE group, in any order,
     groups in random order, idle padding; two calls in a row continue the
-    keystream.  nb = 64 buckets runs half-group workgroups, 200 whole-group
-    ones; trunc drops the last entries of the batch (a short last bucket whose
+    keystream.  nb = 27 buckets runs the speculative-window kernel (at most 32
+    buckets, workgroup columns spread over the XCDs: 27 is no multiple of 8),
+    64 half-group workgroups, 200 whole-group ones; trunc drops the last entries of the batch (a short last bucket whose
     slots still fall in both halves of its group).  Checked against the
     oracle, every session that ran and every state; slots outside the batch
     keep their state."""

@@ -18,7 +18,7 @@
 #define ZRC4_HALF 1   // A/B knob: 0 runs few-group range batches on whole-group workgroups too
 #endif
 #ifndef ZRC4_WIN_MAX_GROUPS
-#define ZRC4_WIN_MAX_GROUPS 16   // aligned range and grouped batches of at most this many groups run
+#define ZRC4_WIN_MAX_GROUPS 32   // aligned range and grouped batches of at most this many groups run
                                  // 16 lanes per stream (crypt_win_kernel, zrc4_win.hpp); 0 = never
 #endif
 
