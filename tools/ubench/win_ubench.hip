@@ -650,6 +650,7 @@ win12_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uin
 
 
 
+
 // v7: one stream per wave, W = 64 (zrc4::win64_windows).
 __global__ void __launch_bounds__(64)
 win7_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,

@@ -4,6 +4,7 @@
 //    store behind the b / marker round trip: shipped as zrc4::win_windows v17)
 //   mode 11 = C: v17 + S0[t] issued under the marker round trip (waits by count)
 //   mode 12 = D: C + v_cmpx for the commit exec
+//   (F, waiting only for a_l at the top and for S_final[t] / M[t] mid-scan, was wrong and slower: removed)
 //   (E, the duplicate rule from a 64-bit ballot shifted to the stream's row with the d-rule OR
 //    chain under the marker round trip, was slower and not bit-exact as written: removed)
 #pragma once
