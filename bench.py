@@ -9,12 +9,18 @@ of the chosen workload:
   cfg2 (default, BASELINE configs[1]): 4 096 sessions x 1 KiB per GPU
   cfg3: 65 536 x 256 B   cfg4: 1 024 x 64 KiB   cfg5: 524 288 x 1 KiB
 
-Multi-GPU: one process per GPU (torchrun), sessions shard across ranks with no
+Multi-GPU: one process per GPU, sessions shard across ranks with no
 collective on the data path; each rank runs the same per-GPU
 batch over its own global session ids -> "scaling": "weak"; with --strong the
 workload's sessions are the whole job and ranks split them (BASELINE
 configs[4]: --workload cfg5 --strong).  torch.distributed
-is used only for the start/stop barrier and the max-over-ranks time.
+is used only for the start/stop barrier and the max-over-ranks time.  Ranks
+come from torchrun's environment, or -- `--gpus N` with no WORLD_SIZE set --
+bench.py starts its own N rank processes (self_launch: child processes with
+RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*; the parent never touches the GPU).
+Which curve a line is: config.curve.  The weak cfg2 line also carries the
+strong configs[4] split measured in the same job ("configs4_strong": 524 288
+x 1 KiB over the same ranks), so a 1/2/4/8 sweep yields both curves.
 
 HBM honesty: each rank rotates over R distinct batches (distinct sessions,
 states and payload buffers) totalling >= --footprint-mib (default 640 MiB, i.e.
@@ -154,6 +160,14 @@ class GpuRunner:
     def check(self) -> None:
         self.ctx.sync(self.stream)
 
+    def close(self) -> None:
+        """Free the batches and the arena (before the companion measurement)."""
+        self.torch.cuda.synchronize()
+        self._args = []
+        self.payload = self.off = self.len = self.ids = None
+        self.ctx.close()
+        self.torch.cuda.empty_cache()
+
     def make_events(self, k: int, every: int = 16):
         """The HIP events of timed_steps, created BEFORE the timed region
         (creating one costs host time that is not part of a step)."""
@@ -190,20 +204,33 @@ class GpuRunner:
         return [a.elapsed_time(b) / m for a, b, m in zip(marks, marks[1:], counts)]
 
 
-def run_bench(args, ws, rank, local, backend="nccl", make_runner=None):
+def ensure_process_group(ws, local, backend):
+    """One process group per job (RCCL on the GPU box, gloo in the CPU tests);
+    returns True when this call created it."""
+    import torch
+    import torch.distributed as dist
+    if ws <= 1 or dist.is_initialized():
+        return False
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return True
+
+
+def run_bench(args, ws, rank, local, backend="nccl", make_runner=None, own_pg=True):
     """Shared orchestration (GPU bench and the gloo CPU test): W untimed steps,
     barrier + sync, K timed steps, sync + barrier, max over ranks.  Sessions
-    shard across ranks by global id (shard_first); no data-path collective."""
+    shard across ranks by global id (shard_first); no data-path collective.
+    own_pg: tear the process group down at the end (main() keeps it for the
+    configs[4] companion measurement and tears it down itself)."""
     import torch
     import torch.distributed as dist
 
     on_gpu = backend == "nccl"
-    if ws > 1:
-        if on_gpu:
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+    ensure_process_group(ws, local, backend)
+    seen_ws = dist.get_world_size() if dist.is_initialized() else 1
     S_job, L = CONFIG_SHAPES[args.workload]
     # --strong: the workload's sessions are the WHOLE job (BASELINE configs[4]:
     # 524 288 sessions sharded across the GPUs); otherwise every rank runs it
@@ -248,6 +275,8 @@ def run_bench(args, ws, rank, local, backend="nccl", make_runner=None):
     if rank == 0:
         total_payload = (args.steps * S_job * L) if args.strong else (ws * args.steps * S * L)
         res = build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload)
+        res["config"]["world_size_seen"] = seen_ws
+        res["config"]["dist_backend"] = (dist.get_backend() if dist.is_initialized() else "none (one process)")
         # per-GPU achieved B/t separates a latency bound from a scaling bug
         B = algorithmic_bytes(S, L)
         res["per_gpu"] = [{"rank": r, "payload_gibs": round(args.steps * S * L / e / GIB, 3),
@@ -260,12 +289,14 @@ def run_bench(args, ws, rank, local, backend="nccl", make_runner=None):
             res["cpu_baseline"] = None
     if ws > 1:
         dist.barrier()
-        dist.destroy_process_group()
+        if own_pg:
+            dist.destroy_process_group()
     return res, runner
 
 
 CONFIG_SHAPES = {"cfg2": (4096, 1024), "cfg3": (65536, 256), "cfg4": (1024, 65536),
                  "cfg5": (524288, 1024)}
+COMPANION_BASES = {"cfg2"}     # workloads whose line carries the configs[4] companion
 CONFIG_TEXT = {"cfg2": "4096 sessions x 1 KiB per GPU (BASELINE configs[1])",
                "cfg3": "65536 sessions x 256 B per GPU (BASELINE configs[2])",
                "cfg4": "1024 sessions x 64 KiB per GPU (BASELINE configs[3])",
@@ -306,6 +337,9 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
                            else "per-GPU batch replicated over ranks' own sessions (weak)"),
                    "footprint_mib_per_gpu": round(R * S * (L + 256) / 2**20, 1),
                    "parallelism": f"shard{ws} (sessions split across GPUs, no collective)",
+                   "curve": (f"strong: {args.workload}'s {S * ws} sessions split over {ws} GPU(s)" if args.strong
+                             else f"weak: {args.workload} per GPU on each of {ws} GPU(s); the strong configs[4] "
+                                  f"split is 'configs4_strong' (or --workload cfg5 --strong)"),
                    "slot_ids": getattr(args, "ids", "range")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -317,7 +351,7 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
                      "kernel_timing": f"HIP events bracketing {len(kern_ms)} segments of "
                                       f"{args.event_every} back-to-back timed launches (per-launch average)"},
         "latency_ceiling_gibs": {"note": "chain-bound payload rate min(S,131072 resident)*2.4GHz/L_cyc per "
-                                         "stream: L46 = 16 lanes per stream (crypt_win_kernel, <= 16 groups), "
+                                         "stream: L46 = 16 lanes per stream (crypt_win_kernel, <= 32 groups), "
                                          "L96 = one lane per stream, L130 = one lane at 8 waves/CU",
                                  "L46": round(latency_ceiling(S, L, 46), 1),
                                  "L96": round(latency_ceiling(S, L, 96), 1),
@@ -379,21 +413,32 @@ def cgroup_cpu_quota():
         return None
 
 
+def usable_cpus():
+    """CPUs this process can run on at once: the affinity mask, capped by the
+    cgroup CPU quota (a 16-CPU quota on a 256-core host is 16, not 256).
+    Returns (usable, affinity_cores, quota)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    usable = aff if quota is None else max(1, min(aff, math.ceil(quota)))
+    return usable, aff, quota
+
+
 def cpu_baseline(args, S, L):
     """The oracle restatement (a -O3 C port of rc4_encryption.h:74-93) timed on
     this host on a bounded sample of the same workload (same keys, payload and
     pre-advance as rank 0's first batch): 1 thread (the reference's single
-    event-loop thread), then one worker per core in this process's affinity
-    mask, each re-crypting its round-robin share for the whole window (one
-    thread start per worker).  Reported, not optimised against."""
+    event-loop thread), then one worker per CPU the process can use at once
+    (usable_cpus: affinity mask capped by the cgroup quota), each re-crypting
+    its round-robin share for the whole window (one thread start per worker).
+    Reported, not optimised against."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle  # cpu_baseline leg only
     from zsummerx_amd import synth
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except Exception:
-        cores = os.cpu_count() or 1
+    cores, aff, quota = usable_cpus()
     if args.cpu_threads > 0:
         cores = min(cores, args.cpu_threads)
     w = synth.make(0, S, L, threads=8)
@@ -409,11 +454,11 @@ def cpu_baseline(args, S, L):
 
     one = rate(1)
     many = rate(cores) if cores > 1 else one
-    return {"value": round(many, 4), "unit": "GiB/s", "cores": cores, "kind": "port",
+    return {"value": round(many, 4), "unit": "GiB/s", "cores": cores, "threads": cores, "kind": "port",
             "value_1thread": round(one, 4), "hardware_concurrency": os.cpu_count(),
-            "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "affinity_cores": aff, "cgroup_cpu_quota": quota,
             "sample": f"{args.workload} batch ({S} x {L} B) re-crypted for {win:.1f} s windows, median of {reps}: "
-                      f"1 thread, then {cores} threads (every core in the affinity mask)"}
+                      f"1 thread, then {cores} threads (min(affinity {aff}, ceil(cgroup quota {quota})))"}
 
 
 # ------------------------------------------------------- host-inclusive rate
@@ -691,14 +736,127 @@ def parse(argv=None):
                    help="measure the device-side proto4z framing scan instead (DESIGN.md), one JSON line")
     p.add_argument("--zero-copy", action="store_true",
                    help="with --host-inclusive: run the kernels directly on the pinned host buffer")
+    p.add_argument("--companion-workload", choices=sorted(CONFIG_SHAPES) + ["none"], default="cfg5",
+                   help="with the default weak cfg2 line: also measure this workload split over the same ranks "
+                        "(strong scaling, BASELINE configs[4]) as 'configs4_strong'; none disables")
+    p.add_argument("--companion-steps", type=int, default=100)
+    p.add_argument("--companion-warmup", type=int, default=120)
     p.add_argument("--chunks", type=int, default=8)
     p.add_argument("--streams", type=int, default=3)
     return p.parse_args(argv)
 
 
-def main(argv=None):
-    args = parse(argv)
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(argv, n: int, entry=None, timeout: float | None = None) -> int:
+    """`--gpus N` without torchrun: start N rank processes of `entry` (default
+    this file) with the environment torchrun would give them (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), relay rank
+    0's JSON line to stdout and return the first non-zero exit code (0 when
+    every rank succeeded).  The parent never touches the GPU and never execs:
+    the ranks are child processes.  When one rank fails the others are
+    terminated (they would otherwise wait at the barrier)."""
+    import subprocess
+    import tempfile
+    entry = str(entry or Path(__file__).resolve())
+    port = free_port()
+    out0 = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, entry, *argv], env=env,
+                                      stdout=out0 if r == 0 else 2))      # other ranks: stdout -> our stderr
+    log(f"[self_launch] {n} ranks of {Path(entry).name}, master 127.0.0.1:{port}, pids {[p.pid for p in procs]}")
+    deadline = None if timeout is None else time.time() + timeout
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad or all(c is not None for c in codes):
+            rc = bad[0] if bad else 0
+            break
+        if deadline is not None and time.time() > deadline:
+            rc = 124
+            break
+        time.sleep(0.1)
+    if rc:
+        log(f"[self_launch] a rank exited with {rc}: stopping the others")
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    out0.seek(0)
+    lines = [ln for ln in out0.read().splitlines() if ln.startswith("{")]
+    if not rc and not lines:
+        log("[self_launch] rank 0 printed no JSON line")
+        rc = 1
+    if lines:
+        print(lines[-1], flush=True)
+    return rc
+
+
+def companion_strong(args, ws, rank, local, backend="nccl", make_runner=None):
+    """BASELINE configs[4] -- 524 288 sessions x 1 KiB split over the job's
+    ranks (strong scaling) -- measured in the same job as the weak cfg2 line,
+    so one 1/2/4/8 sweep yields both curves.  Same barrier / max-over-ranks
+    timing; steady-state warmup (the clock dips over the first ~100 cfg5
+    launches)."""
+    c = argparse.Namespace(**vars(args))
+    c.workload, c.strong, c.cpu_seconds, c.ids = args.companion_workload, True, 0.0, "range"
+    c.steps = max(args.steps, args.companion_steps)
+    c.warmup = max(args.warmup, args.companion_warmup)
+    res, runner = run_bench(c, ws, rank, local, backend, make_runner, own_pg=False)
+    if hasattr(runner, "close"):
+        runner.close()
+    if res is None:
+        return None
+    keep = ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "scaling")
+    out = {k: res[k] for k in keep}
+    out["config"] = {k: res["config"][k] for k in ("workload", "sessions_per_gpu", "global_sessions_per_step",
+                                                   "rotation_batches_per_gpu", "world_size_seen", "curve")}
+    out["roofline"] = {k: res["roofline"][k] for k in ("achieved", "peak", "unit", "frac", "kernel",
+                                                       "algorithmic_bytes_per_launch", "kernel_avg_us")}
+    out["per_gpu"] = res["per_gpu"]
+    return out
+
+
+def rank_main(args, backend="nccl", make_runner=None):
+    """One rank of the bench (torchrun's, self_launch's or the only one)."""
+    import torch.distributed as dist
     ws, rank, local = dist_env()
+    if ws != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE")
+    res, runner = run_bench(args, ws, rank, local, backend, make_runner, own_pg=False)
+    if hasattr(runner, "close"):
+        runner.close()
+    del runner
+    if args.companion_workload != "none" and not args.strong and args.workload in COMPANION_BASES \
+            and getattr(args, "ids", "range") == "range":
+        comp = companion_strong(args, ws, rank, local, backend, make_runner)
+        if rank == 0:
+            res["configs4_strong"] = comp
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    return res
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
     if args.host_inclusive:
         print(json.dumps(host_inclusive(args)), flush=True)
         return
@@ -708,11 +866,9 @@ def main(argv=None):
     if args.frame:
         print(json.dumps(frame_bench(args)), flush=True)
         return
-    if ws != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE")
-    res, _ = run_bench(args, ws, rank, local)
-    if rank == 0:
-        print(json.dumps(res), flush=True)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(argv, args.gpus))
+    rank_main(args)
 
 
 if __name__ == "__main__":

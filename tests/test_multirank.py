@@ -9,6 +9,7 @@ each rank's ciphertext equals the single-process result for those global
 sessions; rank 0 reports the whole-job aggregate from the MAX rank time.
 """
 import hashlib
+import json
 import os
 import socket
 import sys
@@ -18,6 +19,7 @@ import pytest
 import torch.multiprocessing as mp
 
 from conftest import ROOT
+from oracle_runner import OracleRunner
 
 sys.path.insert(0, str(ROOT))
 
@@ -26,56 +28,6 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
-
-
-class OracleRunner:
-    """Runner with the GpuRunner interface, backed by the CPU oracle."""
-
-    def __init__(self, S, L, R, first):
-        import pyoracle
-        from zsummerx_amd import synth
-        self.S, self.L, self.R, self.first = S, L, R, first
-        w = synth.make(first, S * R, L)
-        self.w = w
-        self.ob = pyoracle.Batch(S * R)
-        self.ob.make_sbox(w.keys, w.key_off, w.key_len)
-        self.ob.crypt(np.zeros(1000, dtype=np.uint8), np.zeros(S * R, dtype=np.uint64), w.adv)
-        self.steps_done = []
-
-    def step(self, i):
-        import pyoracle  # noqa: F401
-        b = i % self.R
-        sl = slice(b * self.S, (b + 1) * self.S)
-        # crypt only batch b's sessions (others keep their state)
-        sub_off = self.w.off.copy()
-        sub_len = np.zeros_like(self.w.length)
-        sub_len[sl] = self.w.length[sl]
-        self.ob.crypt(self.w.payload, sub_off, sub_len)
-        self.steps_done.append(i)
-
-    def sync(self):
-        pass
-
-    def check(self):
-        pass
-
-    # bench.GpuRunner's timing interface: events made before the timed
-    # region, launches, then per-segment ms per step
-    def make_events(self, k, every=16):
-        return [None] * (-(-k // every) + 1)
-
-    def launch_steps(self, first, k, every, marks):
-        import time
-        for seg, d in enumerate(range(0, k, every)):
-            t0 = time.perf_counter()
-            m = min(every, k - d)
-            for i in range(first + d, first + d + m):
-                self.step(i)
-            marks[seg] = (time.perf_counter() - t0) * 1e3 / m
-
-    @staticmethod
-    def segment_ms(k, every, marks):
-        return [v for v in marks if v is not None]
 
 
 def _worker(rank, ws, port, q, workload, steps, warmup, footprint, strong=False):
@@ -161,3 +113,53 @@ def test_two_rank_gloo_strong_scaling():
     total = steps * 512 * 64                                   # the job once, not per rank
     expect = total / (res["ms_per_step"] * steps * 1e-3) / 2**30
     assert abs(res["value"] - expect) <= 0.02 * expect + 2e-3
+
+
+@pytest.mark.timeout(300)
+def test_self_launch_two_ranks(capsys):
+    """`python bench.py --gpus 2` without torchrun: bench.self_launch starts
+    the two rank processes itself (here tests/bench_child_cpu.py: the same
+    rank_main over gloo with the oracle runner) and relays rank 0's line,
+    which names the weak curve, the world size the process group saw, one
+    per_gpu entry per rank, and the strong configs[4]-style companion split
+    over the same ranks."""
+    import bench
+    argv = ["--gpus", "2", "--workload", "tiny", "--steps", "3", "--warmup", "1", "--footprint-mib", "0",
+            "--cpu-seconds", "0", "--companion-workload", "tiny2", "--companion-steps", "2",
+            "--companion-warmup", "1"]
+    rc = bench.self_launch(argv, 2, entry=ROOT / "tests" / "bench_child_cpu.py", timeout=240)
+    out = capsys.readouterr().out
+    assert rc == 0, out
+    res = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+    assert res["n_gpus"] == 2 and res["scaling"] == "weak"
+    assert res["config"]["world_size_seen"] == 2 and res["config"]["dist_backend"] == "gloo"
+    assert res["config"]["curve"].startswith("weak")
+    assert [g["rank"] for g in res["per_gpu"]] == [0, 1]
+    comp = res["configs4_strong"]
+    assert comp["n_gpus"] == 2 and comp["scaling"] == "strong"
+    assert comp["config"]["sessions_per_gpu"] == 256 and comp["config"]["global_sessions_per_step"] == 512
+    assert comp["config"]["world_size_seen"] == 2
+    assert [g["rank"] for g in comp["per_gpu"]] == [0, 1]
+    expect = comp["steps"] * 512 * 64 / (comp["ms_per_step"] * comp["steps"] * 1e-3) / 2**30
+    assert abs(comp["value"] - expect) <= 0.02 * expect + 2e-3
+
+
+@pytest.mark.timeout(120)
+def test_self_launch_reports_a_failing_rank(capsys):
+    """A rank that fails makes the job fail (non-zero exit), and the other
+    rank is stopped rather than left waiting at the barrier."""
+    import bench
+    argv = ["--gpus", "2", "--workload", "no-such-shape"]
+    rc = bench.self_launch(argv, 2, entry=ROOT / "tests" / "bench_child_cpu.py", timeout=100)
+    assert rc != 0
+
+
+def test_usable_cpus_caps_affinity_by_quota(monkeypatch):
+    import bench
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(256)))
+    monkeypatch.setattr(bench, "cgroup_cpu_quota", lambda: 16.0)
+    assert bench.usable_cpus() == (16, 256, 16.0)
+    monkeypatch.setattr(bench, "cgroup_cpu_quota", lambda: 2.5)
+    assert bench.usable_cpus()[0] == 3
+    monkeypatch.setattr(bench, "cgroup_cpu_quota", lambda: None)
+    assert bench.usable_cpus()[0] == 256
