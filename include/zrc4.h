@@ -62,6 +62,8 @@ extern "C" {
 #define ZRC4_ERR_HIP (-6)
 #define ZRC4_ERR_GROUP (-7)    /* zrc4_crypt_grouped: a bucket mixes slot groups */
 #define ZRC4_ERR_INTERNAL (-8) /* kernel self-check failed (LDS layout) */
+#define ZRC4_ERR_STATE (-9)    /* zrc4_ks: the slot's stream position was lost by a failed
+                                  crypt; reseed (zrc4_ks_make_sbox) or copy into it */
 
 /* Slots are grouped 256 to a 64 KiB device image (the LDS image of one
  * workgroup); capacity is rounded up to a multiple of this. */

@@ -68,12 +68,17 @@ public:
     }
     static uint32_t local(uint32_t slot) { return slot % kChunk; }
 
-    uint32_t acquire()
+    // A slot for a new RC4Encryption.  *recycled: the slot comes back from a
+    // destroyed instance and still holds that stream's state; its new owner
+    // resets it lazily (RC4Encryption::prepare), so a destructor makes no GPU
+    // call and a new owner that starts with makeSBox pays for no reset.
+    uint32_t acquire(bool *recycled)
     {
         std::lock_guard<std::mutex> g(mu_);
         if (!free_.empty()) {
             const uint32_t s = free_.back();
             free_.pop_back();
+            *recycled = true;
             return s;
         }
         if (next_ == (uint64_t)chunks_.size() * kChunk) {
@@ -86,16 +91,21 @@ public:
             chunks_.push_back(c);
             ks_.push_back(k);
         }
+        *recycled = false;                 // a fresh slot holds the empty-key state
         return (uint32_t)next_++;
     }
-    // The slot goes back to the empty-key state (identity box, x = y = 0:
-    // makeSBox(""), rc4_encryption.h:48-56) so its next owner never sees the
-    // previous stream.
+    // Back to the free list; no GPU call (destructors may run during static
+    // destruction, and a session teardown should not wait on the device).
     void release(uint32_t s)
     {
-        const int rc = zrc4_ks_make_sbox(ks(s), local(s), nullptr, 0);   // identity, ring emptied
         std::lock_guard<std::mutex> g(mu_);
-        if (rc == ZRC4_OK) free_.push_back(s);   // a slot that cannot be reset is not reused
+        free_.push_back(s);
+    }
+    // The empty-key state (identity box, x = y = 0: makeSBox(""),
+    // rc4_encryption.h:48-56), ring emptied.
+    static void reset(uint32_t s)
+    {
+        zrc4_throw(zrc4_ks_make_sbox(instance().ks(s), local(s), nullptr, 0), "RC4Encryption reset");
     }
     ~Rc4Arena()
     {
@@ -122,25 +132,26 @@ private:
 
 class RC4Encryption {
 public:
-    RC4Encryption() : slot_(Rc4Arena::instance().acquire()) {}
+    RC4Encryption() : slot_(Rc4Arena::instance().acquire(&stale_)) {}
     ~RC4Encryption()
     {
         if (slot_ != kNoSlot) Rc4Arena::instance().release(slot_);
     }
     // A value type like the reference (an int[256] + x + y member block): a
     // copy owns its own slot holding the same state.
-    RC4Encryption(const RC4Encryption &o) : slot_(Rc4Arena::instance().acquire()) { copyState(o); }
+    RC4Encryption(const RC4Encryption &o) : slot_(Rc4Arena::instance().acquire(&stale_)) { copyState(o); }
     RC4Encryption &operator=(const RC4Encryption &o)
     {
         if (this != &o) copyState(o);
         return *this;
     }
-    RC4Encryption(RC4Encryption &&o) noexcept : slot_(o.slot_) { o.slot_ = kNoSlot; }
+    RC4Encryption(RC4Encryption &&o) noexcept : slot_(o.slot_), stale_(o.stale_) { o.slot_ = kNoSlot; }
     RC4Encryption &operator=(RC4Encryption &&o) noexcept
     {
         if (this != &o) {
             if (slot_ != kNoSlot) Rc4Arena::instance().release(slot_);
             slot_ = o.slot_;
+            stale_ = o.stale_;
             o.slot_ = kNoSlot;
         }
         return *this;
@@ -154,15 +165,28 @@ public:
         zrc4_throw(zrc4_ks_make_sbox(Rc4Arena::instance().ks(slot_), Rc4Arena::local(slot_),
                                      reinterpret_cast<const uint8_t *>(obscure.data()), obscure.size()),
                    "RC4Encryption::makeSBox");
+        stale_ = false;
     }
 
     // rc4_encryption.h:74-93 -- in place; length <= 0 does nothing.
     void encryption(unsigned char *data, int length)
     {
         if (length <= 0) return;
+        prepare();
         const uint32_t id = Rc4Arena::local(slot_), n = (uint32_t)length;
         uint8_t *d = data;
         zrc4_throw(zrc4_ks_crypt(Rc4Arena::instance().ks(slot_), &id, &d, &n, 1), "RC4Encryption::encryption");
+    }
+
+    // A recycled slot still holds its previous owner's stream until this
+    // object seeds it: used before makeSBox, it starts from the empty-key
+    // state like a fresh slot (the reset happens here, once).
+    void prepare() const
+    {
+        if (stale_) {
+            Rc4Arena::reset(slot_);
+            stale_ = false;
+        }
     }
 
     uint32_t slot() const { return slot_; }
@@ -172,11 +196,14 @@ private:
     // device state + the keystream already buffered for the source
     void copyState(const RC4Encryption &o)
     {
+        o.prepare();
         Rc4Arena &a = Rc4Arena::instance();
         zrc4_throw(zrc4_ks_copy(a.ks(slot_), Rc4Arena::local(slot_), a.ks(o.slot_), Rc4Arena::local(o.slot_)),
                    "RC4Encryption copy");
+        stale_ = false;
     }
     uint32_t slot_;
+    mutable bool stale_ = false;
 };
 
 // Batched hook path: collect (slot, buffer, len) for one event-loop
@@ -188,6 +215,15 @@ private:
 class Rc4Batch {
 public:
     explicit Rc4Batch(zrc4_ks *ks) : ks_(ks) {}
+    // An RC4Encryption of this batch's reservoir (a recycled slot used before
+    // its makeSBox is reset first, as RC4Encryption::encryption does).
+    void add(const RC4Encryption &r, unsigned char *data, unsigned len)
+    {
+        if (!len) return;
+        r.prepare();
+        add(Rc4Arena::local(r.slot()), data, len);
+    }
+    // A raw slot of the reservoir's chunk that the caller has seeded.
     void add(uint32_t slot, unsigned char *data, unsigned len)
     {
         if (!len) return;

@@ -198,6 +198,16 @@ def test_crypt_host_scattered_ids_grouped(built, torch_cuda):
             c.crypt_host(buf, np.arange(10, dtype=np.uint64) * 16, np.full(10, 16, dtype=np.uint32), ids=dup)
         assert ei.value.code == -1                 # ZRC4_ERR_INVALID_ARG
         assert c.get_state(int(dup[2])) == before and not buf.any()
+        # an id past the arena -- ZRC4_IDLE_SLOT (0xFFFFFFFF) included, which
+        # the kernels would skip as padding -- is refused, nothing crypted
+        for bad in (cap, 0xFFFFFFFF):
+            bid = ids[:10].copy()
+            bid[7] = bad
+            before = c.get_state(int(bid[2]))
+            with pytest.raises(ZRC4Error) as ei:
+                c.crypt_host(buf, np.arange(10, dtype=np.uint64) * 16, np.full(10, 16, dtype=np.uint32), ids=bid)
+            assert ei.value.code == -5             # ZRC4_ERR_SLOT_RANGE
+            assert c.get_state(int(bid[2])) == before and not buf.any()
 
 
 def test_batch_whole_group_ids(ctx, batch_small):

@@ -21,6 +21,7 @@ ERRORS = {
     -6: "ZRC4_ERR_HIP",
     -7: "ZRC4_ERR_GROUP",
     -8: "ZRC4_ERR_INTERNAL",
+    -9: "ZRC4_ERR_STATE",
 }
 IDLE_SLOT = 0xFFFFFFFF
 

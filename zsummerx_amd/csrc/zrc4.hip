@@ -449,9 +449,12 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
     if (!c) return ZRC4_ERR_INVALID_ARG;
     if (n == 0) return ZRC4_OK;
     if (!off || !len || (payload_bytes && !payload)) return ZRC4_ERR_INVALID_ARG;
-    for (uint32_t i = 0; i < n; ++i)
+    for (uint32_t i = 0; i < n; ++i) {
         if (len[i] && (off[i] > payload_bytes || len[i] > payload_bytes - off[i]))
             return ZRC4_ERR_INVALID_ARG;
+        // (ZRC4_IDLE_SLOT included: the kernels would skip it as padding)
+        if (ids && ids[i] >= c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    }
     int rc = set_device(c);
     if (rc) return rc;
     // Several arbitrary ids: bucket them by 256-slot group here (the
@@ -596,6 +599,7 @@ const char *zrc4_strerror(int code)
     case ZRC4_ERR_HIP: return "HIP runtime error";
     case ZRC4_ERR_GROUP: return "zrc4_crypt_grouped: a 256-entry bucket mixes slot groups";
     case ZRC4_ERR_INTERNAL: return "internal error: S-box image not at LDS offset 0";
+    case ZRC4_ERR_STATE: return "slot state lost (a failed reservoir crypt): reseed it with zrc4_ks_make_sbox or zrc4_ks_copy";
     default: return "unknown zrc4 error";
     }
 }

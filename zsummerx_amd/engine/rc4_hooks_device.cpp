@@ -495,7 +495,7 @@ private:
                 const Level &L = level_[spans[i].slot];
                 if (L.gen - L.use < spans[i].len && L.pend > L.gen) wait = true;
             }
-            if (!wait) break;
+            if (!wait || !inFlight_) break;      // nothing queued: the span goes to the tail path
             ++refillWaits_;
             if ((rc = commitOldest(true)) != ZRC4_OK) return rc;
         }
@@ -584,10 +584,29 @@ private:
         if (rs_.empty()) return ZRC4_OK;
         buildGrouped(R.t, rs_);
         int rc = zrc4_crypt_grouped(ctx_, R.t.ids.p, base_, R.t.off.p, R.t.len.p, R.t.n, sB_);
-        if (rc != ZRC4_OK) return rc;
-        if (hipEventRecord(R.ev, sB_) != hipSuccess) return ZRC4_ERR_HIP;
-        ++inFlight_;
+        if (rc != ZRC4_OK) {
+            // nothing queued: the levels go back (pend > gen with no refill in
+            // flight would make cryptReservoir wait for bytes that never come)
+            for (const Entry &e : rs_) level_[e.slot].pend -= e.len;
+            R.ends.clear();
+            return rc;
+        }
         ++refillLaunches_;
+        if (hipEventRecord(R.ev, sB_) != hipSuccess) {
+            // the refill is queued but cannot be tracked: wait for stream B
+            // and commit its bytes now
+            if (hipStreamSynchronize(sB_) != hipSuccess) return ZRC4_ERR_HIP;
+            for (const auto &se : R.ends) {
+                Level &L = level_[se.first];
+                if (se.second > L.gen) {
+                    refillBytes_ += se.second - L.gen;
+                    L.gen = se.second;
+                }
+            }
+            R.ends.clear();
+            return zrc4_poll_faults(ctx_);
+        }
+        ++inFlight_;
         if (debugSyncRefill_) return drainRefills();
         return ZRC4_OK;
     }
