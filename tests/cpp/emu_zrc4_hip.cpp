@@ -11,6 +11,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -60,11 +61,14 @@ int zrc4_crypt(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_
     return ZRC4_OK;
 }
 // Same contract checks as crypt_kernel<kGrouped>: a bucket's busy entries
-// must share one group (else the bucket is skipped and ZRC4_ERR_GROUP reported).
+// must share one group, and no other bucket of the call may name that group
+// (else the bucket is skipped and ZRC4_ERR_GROUP reported; here the first
+// bucket to name a group keeps it).
 int zrc4_crypt_grouped(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const uint64_t *off,
                        const uint32_t *len, uint32_t n, void *)
 {
     int rc = ZRC4_OK;
+    std::vector<uint32_t> held;
     for (uint32_t b = 0; b < n; b += 256) {
         const uint32_t e = b + 256 < n ? b + 256 : n;
         uint32_t gmin = 0xFFFFFFFFu, gmax = 0;
@@ -77,6 +81,13 @@ int zrc4_crypt_grouped(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, const
         if (gmin != 0xFFFFFFFFu && gmin != gmax) {
             rc = ZRC4_ERR_GROUP;
             continue;
+        }
+        if (gmin != 0xFFFFFFFFu) {
+            if (std::find(held.begin(), held.end(), gmin) != held.end()) {
+                rc = ZRC4_ERR_GROUP;
+                continue;
+            }
+            held.push_back(gmin);
         }
         for (uint32_t i = b; i < e; ++i)
             if (len[i] && ids[i] != ZRC4_IDLE_SLOT) oracle_encryption(&c->st[ids[i]], payload + off[i], (long)len[i]);

@@ -552,6 +552,78 @@ def test_grouped_ids_mixed_bucket_is_refused(built, torch_cuda):
         assert got[256 * 32: 257 * 32].tobytes() == ks
 
 
+@pytest.mark.parametrize("nb", [20, 100, 200])
+def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb):
+    """The cross-bucket half of the zrc4_crypt_grouped contract: two buckets
+    of one call name the same group (disjoint slots of it).  The call reports
+    ZRC4_ERR_GROUP; every other bucket is bit-exact (payload and states); in
+    the contested group every entry is all-or-nothing -- crypted exactly as
+    the oracle does with its state advanced, or untouched with its state
+    unchanged -- never raced.  nb = 20: the window kernel (one claim per
+    dword column), 100: half-group workgroups, 200: whole-group workgroups."""
+    torch = torch_cuda
+    from zsummerx_amd._capi import IDLE_SLOT
+    rng = np.random.default_rng(500 + nb)
+    G = 256
+    cap = 256 * G
+    keys = rng.integers(0, 256, 16 * cap, dtype=np.uint8)
+    koff = np.arange(cap, dtype=np.uint64) * 16
+    klen = np.full(cap, 16, dtype=np.uint32)
+    ob = pyoracle.Batch(cap)
+    ob.make_sbox(keys, koff, klen)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    s = torch.cuda.current_stream()
+    groups = rng.permutation(G)[:nb - 1]
+    dup_a, dup_b = 3, nb - 2                           # buckets dup_a and dup_b both take group groups[dup_a]
+    ids = np.full(256 * nb, IDLE_SLOT, dtype=np.uint32)
+    contested = int(groups[dup_a])
+    half = rng.permutation(256)
+    for b in range(nb):
+        if b == dup_b:
+            ids[256 * b: 256 * b + 128] = contested * 256 + half[128:]
+        elif b == dup_a:
+            ids[256 * b: 256 * b + 128] = contested * 256 + half[:128]
+        else:
+            g = int(groups[b if b < dup_b else b - 1])
+            k = int(rng.integers(1, 257))
+            ids[256 * b + rng.permutation(256)[:k]] = g * 256 + rng.permutation(256)[:k]
+    busy = ids != IDLE_SLOT
+    L = np.where(busy, rng.integers(1, 500, ids.size), 0).astype(np.uint32)
+    off = np.arange(ids.size, dtype=np.uint64) * 512
+    data = rng.integers(0, 256, ids.size * 512, dtype=np.uint8)
+    with Context(0, cap) as c:
+        c.ksa_range(0, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
+        pay = T(data)
+        c.crypt_grouped(pay, T(off.view(np.int64)), T(L.view(np.int32)), T(ids.view(np.int32)), stream=s)
+        with pytest.raises(ZRC4Error) as ei:
+            c.sync(s)
+        assert ei.value.code == -7                      # ZRC4_ERR_GROUP
+        got = pay.cpu().numpy()
+        crypted = untouched = 0
+        for e in np.flatnonzero(busy):
+            slot, a, z = int(ids[e]), int(off[e]), int(off[e] + L[e])
+            before = ob.state(slot)
+            want = data[a:z].copy()
+            st = ob.st[slot]
+            saved = pyoracle.C.create_string_buffer(bytes(st), pyoracle.C.sizeof(st))
+            pyoracle.lib().oracle_encryption(pyoracle.C.byref(st), pyoracle.C.c_void_p(want.ctypes.data), int(L[e]))
+            after = ob.state(slot)
+            sb, x, y = c.get_state(slot)
+            if slot // 256 != contested:
+                assert np.array_equal(got[a:z], want), (e, slot)
+                assert (sb, x, y) == (bytes(after[0]), after[1], after[2]), slot
+                continue
+            if np.array_equal(got[a:z], want):
+                assert (sb, x, y) == (bytes(after[0]), after[1], after[2]), slot
+                crypted += 1
+            else:
+                assert np.array_equal(got[a:z], data[a:z]), (e, slot)           # untouched, not half-crypted
+                assert (sb, x, y) == (bytes(before[0]), before[1], before[2]), slot
+                pyoracle.C.memmove(pyoracle.C.byref(st), saved, pyoracle.C.sizeof(st))
+                untouched += 1
+        assert untouched >= 1 and crypted + untouched == 256
+
+
 # ------------------------------------------------ full BASELINE-size configs
 def _device_workload(ctx, w, torch):
     dev = "cuda"

@@ -40,6 +40,8 @@ struct zrc4_ctx {
     uint8_t *h_stage;       // pinned
     size_t h_stage_bytes;
     hipStream_t stream;     // private stream for the host entry points
+    unsigned long long *claim;   // grouped launches' (group, part) claim words (zrc4::Claim), zeroed
+    uint32_t epoch;              // the last grouped launch's claim tag
 };
 
 namespace {
@@ -93,6 +95,16 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
 {
     if (n == 0) return ZRC4_OK;
     if (mode == zrc4::kRange && (uint64_t)first_slot + n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    zrc4::Claim cl{nullptr, 0u};
+    if (mode == zrc4::kGrouped) {
+        // a fresh tag per grouped launch; on the 32-bit wrap the words are
+        // zeroed first (stream-ordered before this launch)
+        if (++c->epoch == 0u) {
+            ZRC4_TRY(hipMemsetAsync(c->claim, 0, (size_t)(c->capacity / zrc4::kGroup) * zrc4::kClaimParts * 8u, s));
+            c->epoch = 1u;
+        }
+        cl = zrc4::Claim{c->claim, c->epoch};
+    }
     const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
     const dim3 blk(zrc4::kGroup);
     const bool stream_kernel = mode != zrc4::kGrouped && grid > (uint32_t)c->num_cus;
@@ -104,16 +116,16 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
         const zrc4::FrameArgs fa = fr ? *fr : zrc4::FrameArgs{};
         if (mode == zrc4::kRange && fr)
             hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kRange, true>), wgrid, wblk, 0, s, c->arena, c->xy, ids,
-                               first_slot, payload, off, len, n, c->capacity, c->err, fa);
+                               first_slot, payload, off, len, n, c->capacity, c->err, fa, cl);
         else if (mode == zrc4::kRange)
             hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kRange, false>), wgrid, wblk, 0, s, c->arena, c->xy, ids,
-                               first_slot, payload, off, len, n, c->capacity, c->err, fa);
+                               first_slot, payload, off, len, n, c->capacity, c->err, fa, cl);
         else if (fr)
             hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kGrouped, true>), wgrid, wblk, 0, s, c->arena, c->xy,
-                               ids, first_slot, payload, off, len, n, c->capacity, c->err, fa);
+                               ids, first_slot, payload, off, len, n, c->capacity, c->err, fa, cl);
         else
             hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kGrouped, false>), wgrid, wblk, 0, s, c->arena, c->xy,
-                               ids, first_slot, payload, off, len, n, c->capacity, c->err, fa);
+                               ids, first_slot, payload, off, len, n, c->capacity, c->err, fa, cl);
         return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
     }
     // Few whole groups: half-group workgroups, one per CU (2 waves per CU).
@@ -135,10 +147,10 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
         } else {
             if (fr)
                 hipLaunchKernelGGL((zrc4::crypt_half_kernel<zrc4::kGrouped, true>), hgrid, hblk, 0, s, c->arena,
-                                   c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa);
+                                   c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl);
             else
                 hipLaunchKernelGGL((zrc4::crypt_half_kernel<zrc4::kGrouped, false>), hgrid, hblk, 0, s, c->arena,
-                                   c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa);
+                                   c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl);
         }
         return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
     }
@@ -148,7 +160,7 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
                                ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, *fr);
         else if (mode == zrc4::kGrouped)
             hipLaunchKernelGGL((zrc4::crypt_kernel<zrc4::kGrouped, true>), dim3(grid), blk, 0, s, c->arena, c->xy,
-                               ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, *fr);
+                               ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, *fr, cl);
         else
             return ZRC4_ERR_INVALID_ARG;
         return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
@@ -173,7 +185,7 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
                            first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
     } else if (mode == zrc4::kGrouped) {
         hipLaunchKernelGGL(zrc4::crypt_kernel<zrc4::kGrouped>, dim3(grid), blk, 0, s, c->arena, c->xy, ids,
-                           first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
+                           first_slot, payload, off, len, n, c->capacity, c->err, c->sink, zrc4::FrameArgs{}, cl);
     } else {
         hipLaunchKernelGGL(zrc4::crypt_kernel<zrc4::kIds>, dim3(grid), blk, 0, s, c->arena, c->xy, ids,
                            first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
@@ -240,6 +252,8 @@ int zrc4_create(zrc4_ctx **out, int device, uint32_t capacity)
               hipMalloc(&c->xy, (size_t)c->capacity * sizeof(uint16_t)) == hipSuccess &&
               hipMalloc(&c->sink, zrc4::kSinkBytes) == hipSuccess &&
               hipHostMalloc(&c->err, zrc4::kErrWords * sizeof(uint32_t), hipHostMallocCoherent) == hipSuccess &&
+              hipMalloc(&c->claim, groups * zrc4::kClaimParts * sizeof(unsigned long long)) == hipSuccess &&
+              hipMemset(c->claim, 0, groups * zrc4::kClaimParts * sizeof(unsigned long long)) == hipSuccess &&
               hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     if (!ok) { zrc4_destroy(c); return ZRC4_ERR_OUT_OF_MEMORY; }
     // Fresh slots hold the reference's empty-key state: identity box, x = y = 0
@@ -265,6 +279,7 @@ int zrc4_destroy(zrc4_ctx *c)
     if (c->arena) (void)hipFree(c->arena);
     if (c->xy) (void)hipFree(c->xy);
     if (c->sink) (void)hipFree(c->sink);
+    if (c->claim) (void)hipFree(c->claim);
     if (c->err) (void)hipHostFree(c->err);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);

@@ -51,6 +51,38 @@ __device__ __forceinline__ void latch_fault(uint32_t *err, uint32_t kind)
     __hip_atomic_store(err + kind, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Cross-bucket half of the zrc4_crypt_grouped contract ("no other bucket of
+// the call touches that group", include/zrc4.h): every workgroup of a grouped
+// launch claims the part of its bucket's group it moves -- whole group: part
+// 0; half-group workgroups: the half h; the window kernel: its dword column q
+// -- by one agent-scope 64-bit exchange of (launch epoch << 32 | bucket) into
+// a per-context word per (group, part).  Reading back this launch's epoch
+// means another bucket of the same launch holds that part: the workgroup
+// latches kErrGroup and writes nothing, so no S-box byte, x/y or payload byte
+// is ever raced.  The host gives every grouped launch a fresh non-zero epoch
+// (words are zeroed whenever the 32-bit epoch wraps).  The exchange is issued
+// with the speculative image loads (the first busy id's group), so its round
+// trip hides under theirs; a bucket that breaks the one-group rule may
+// therefore also block the bucket of the group its first busy id names.
+constexpr uint32_t kClaimParts = 64;
+struct Claim {
+    unsigned long long *word;   // [groups][kClaimParts]
+    uint32_t epoch;
+};
+
+__device__ __forceinline__ unsigned long long claim_part(const Claim &cl, uint32_t g, uint32_t part,
+                                                         uint32_t bucket)
+{
+    return __hip_atomic_exchange(cl.word + (size_t)g * kClaimParts + part,
+                                 ((unsigned long long)cl.epoch << 32) | bucket, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool claim_lost(const Claim &cl, unsigned long long old)
+{
+    return (uint32_t)(old >> 32) == cl.epoch;
+}
+
 // The asm addresses S-box bytes absolutely (no base register): S must be the
 // workgroup's first LDS byte.  (uint32_t) of a generic LDS pointer is its
 // offset inside the LDS aperture.
@@ -934,7 +966,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
            const uint32_t *__restrict__ ids, uint32_t first_slot,
            uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
            const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
-           uint32_t *__restrict__ err, uint8_t *__restrict__ sink, const FrameArgs &fr)
+           uint32_t *__restrict__ err, uint8_t *__restrict__ sink, const FrameArgs &fr, const Claim &cl)
 {
     static_assert(!HALF || MODE != kIds, "half-group workgroups run range and grouped batches");
     __shared__ __attribute__((aligned(16))) uint8_t smem[HALF ? kSmemHalf : kSmemDirect];
@@ -1055,12 +1087,17 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         }
         issue_image_asm(ilo, ihi, arena + (size_t)gw * kGroupBytes, vo0);
         const uint16_t xyw = xy[gw * 256u + j];
+        // the claim of this workgroup's part of the group (Claim), by thread 0
+        // on its wave's guess; re-issued below if that wave had no busy entry
+        unsigned long long cold = 0;
+        if (tid == 0 && have) cold = claim_part(cl, gw, HALF ? h : 0u, w);
 #pragma unroll
         for (uint32_t q = 0; q < kPer; ++q) te[q * kLanes + tid] = ZRC4_INVALID;
         if (tid == 0) {
             flag[0] = 0xFFFFFFFFu;
             flag[1] = 0u;
             flag[2] = 0u;
+            flag[3] = 0u;
         }
         __syncthreads();
         if (have && (tid & 63u) == 0u) {
@@ -1101,6 +1138,8 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             issue_image_asm(ilo, ihi, arena + (size_t)g * kGroupBytes, vo0);
             sxy = xy[slot];
         }
+        if (tid == 0 && !have) cold = claim_part(cl, g, HALF ? h : 0u, w);
+        if (tid == 0) flag[3] = claim_lost(cl, cold) ? 1u : 0u;          // read after the fill barrier
         if (!mylen) sxy = 0;
         if constexpr (FRAME) {
             // entries that decrypt nothing are framed by their own thread now
@@ -1158,6 +1197,12 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #pragma unroll
         for (int i = 0; i < 16; ++i) *reinterpret_cast<uint4 *>(S + i * 4096 + vo0) = img[i];
         __syncthreads();
+        if constexpr (MODE == kGrouped) {
+            if (flag[3]) {                               // another bucket of this launch holds the group
+                if (tid == 0) latch_fault(err, kErrGroup);
+                return;
+            }
+        }
     } else {
         if (pre) issue_block_asm(A, msg);
         if (active) gather_column(S, col, arena, slot);
@@ -1204,9 +1249,10 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
              const uint32_t *__restrict__ ids, uint32_t first_slot,
              uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
              const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
-             uint32_t *__restrict__ err, uint8_t *__restrict__ sink, FrameArgs fr = FrameArgs{})
+             uint32_t *__restrict__ err, uint8_t *__restrict__ sink, FrameArgs fr = FrameArgs{},
+             Claim cl = Claim{})
 {
-    crypt_body<MODE, FRAME, false>(arena, xy, ids, first_slot, payload, off, len, n, capacity, err, sink, fr);
+    crypt_body<MODE, FRAME, false>(arena, xy, ids, first_slot, payload, off, len, n, capacity, err, sink, fr, cl);
 }
 
 // Half-group workgroups (kRange / kGrouped, few groups): one per CU;
@@ -1221,9 +1267,10 @@ crypt_half_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                   const uint32_t *__restrict__ ids, uint32_t first_slot,
                   uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
                   const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
-                  uint32_t *__restrict__ err, uint8_t *__restrict__ sink, FrameArgs fr = FrameArgs{})
+                  uint32_t *__restrict__ err, uint8_t *__restrict__ sink, FrameArgs fr = FrameArgs{},
+                  Claim cl = Claim{})
 {
-    crypt_body<MODE, FRAME, true>(arena, xy, ids, first_slot, payload, off, len, n, capacity, err, sink, fr);
+    crypt_body<MODE, FRAME, true>(arena, xy, ids, first_slot, payload, off, len, n, capacity, err, sink, fr, cl);
 }
 
 // ---------------------------------------------------------------------------

@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(64)
 crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const uint32_t *__restrict__ ids,
                  uint32_t first_slot, uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
                  const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity, uint32_t *__restrict__ err,
-                 FrameArgs fr)
+                 FrameArgs fr, Claim cl)
 {
     __shared__ __attribute__((aligned(1024))) uint32_t Mk[kWinStreams * 256];
     __shared__ __attribute__((aligned(kWinRing))) uint8_t Ring[kWinStreams * kWinRing];
@@ -298,6 +298,8 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
+        unsigned long long cold = 0;                                          // the claim of column q (Claim)
+        if (lane == 0) cold = claim_part(cl, gw, q, wg);
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -311,7 +313,8 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             }
         }
         __syncthreads();
-        if (fl[8]) {
+        const bool lost = claim_lost(cl, ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(cold >> 32))) << 32);
+        if (fl[8] || lost) {                                                  // lost: another bucket holds column q
             if (lane == 0) latch_fault(err, kErrGroup);
             return;
         }
