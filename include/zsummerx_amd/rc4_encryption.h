@@ -145,7 +145,7 @@ public:
         if (this != &o) copyState(o);
         return *this;
     }
-    RC4Encryption(RC4Encryption &&o) noexcept : slot_(o.slot_), stale_(o.stale_) { o.slot_ = kNoSlot; }
+    RC4Encryption(RC4Encryption &&o) noexcept : stale_(o.stale_), slot_(o.slot_) { o.slot_ = kNoSlot; }
     RC4Encryption &operator=(RC4Encryption &&o) noexcept
     {
         if (this != &o) {
@@ -202,8 +202,10 @@ private:
                    "RC4Encryption copy");
         stale_ = false;
     }
-    uint32_t slot_;
+    // stale_ is declared (and initialised) before slot_: slot_'s initialiser,
+    // acquire(&stale_), sets it
     mutable bool stale_ = false;
+    uint32_t slot_;
 };
 
 // Batched hook path: collect (slot, buffer, len) for one event-loop
