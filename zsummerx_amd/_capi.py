@@ -6,10 +6,15 @@ calls fail loudly (ZRC4Error), they never drop to a CPU path.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 _PKG = Path(__file__).resolve().parent
 LIB_PATH = _PKG / "libzrc4.so"
+# A/B validation only: run the suite against an in-tree variant build
+# (zsummerx_amd/libzrc4_<name>.so from zsummerx_amd.build.build_variant)
+if os.environ.get("ZSX_ZRC4_VARIANT"):
+    LIB_PATH = _PKG / f"libzrc4_{os.environ['ZSX_ZRC4_VARIANT']}.so"
 
 ZRC4_OK = 0
 ERRORS = {
