@@ -568,7 +568,8 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr uint32_t kSinkSlot = 256;                 // bytes of sink per thread (128-B line + offsets)
 // crypt_stream2_kernel's 512 threads: slots past the timing build's stamps
-constexpr uint32_t kSink2Off = ZRC4_TIMING ? (128u << 10) : 0u;
+// (stream2_stamp: 256 KiB of per-wave stamps, then clocks and HW ids)
+constexpr uint32_t kSink2Off = ZRC4_TIMING ? (320u << 10) : 0u;
 constexpr uint32_t kSinkBytes = kSink2Off + 2u * kGroup * kSinkSlot;   // per context, shared by all workgroups
 
 // line = blocks at b0 (16 B x 4) and b1 (16 B x 4)
@@ -1635,6 +1636,31 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 // ---------------------------------------------------------------------------
 constexpr uint32_t kStream2Threads = 2u * kGroup;
 
+// crypt_stream2_kernel (ZRC4_TIMING): lane 0 of EVERY wave stamps event i
+// (0 entry, 1 + 2r / 2 + 2r round r's keystream start / end, 15 exit) as
+// s_memrealtime into sink[(wg * 8 + wave) * 16 + i] (256 workgroups); entry /
+// exit shader clocks at sink + 256 KiB, HW_ID / XCC_ID at sink + 288 KiB
+// (tools/stream_timeline.py --s2).
+__device__ __forceinline__ void stream2_stamp(uint8_t *sink, uint32_t i)
+{
+#if ZRC4_TIMING
+    const uint32_t wave = threadIdx.x >> 6, slot = blockIdx.x * 8u + wave;
+    if ((threadIdx.x & 63u) == 0u && blockIdx.x < 256u && i < 16u) {
+        reinterpret_cast<uint64_t *>(sink)[slot * 16u + i] = __builtin_amdgcn_s_memrealtime();
+        if (i == 0u || i == 15u)
+            reinterpret_cast<uint64_t *>(sink + (256u << 10))[slot * 2u + (i ? 1u : 0u)] = __builtin_amdgcn_s_memtime();
+        if (i == 0u) {
+            uint32_t hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
+                         : "=s"(hw), "=s"(xcc));
+            uint32_t *o = reinterpret_cast<uint32_t *>(sink + (288u << 10)) + slot * 2u;
+            o[0] = hw;
+            o[1] = xcc;
+        }
+    }
+#endif
+}
+
 __device__ __forceinline__ void lds_to_image2_asm(uint8_t *img, uint32_t tid, uint32_t lbase)
 {
     u32x32 d0, d1;
@@ -1715,7 +1741,7 @@ crypt_stream2_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uin
     const uint32_t G = gridDim.x;
     uint8_t *sk = sink + kSink2Off + (size_t)t * kSinkSlot;
     const uint32_t g0 = first_slot >> 8;
-    stream_stamp(sink, 0);
+    stream2_stamp(sink, 0);
     uint32_t k_t = 0;
     bool p_async = false;
 
@@ -1784,7 +1810,7 @@ crypt_stream2_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uin
                 __builtin_amdgcn_s_setprio(1);
         }
 #endif
-        stream_stamp(sink, 1u + 2u * k_t);
+        stream2_stamp(sink, 1u + 2u * k_t);
         if (active) {
             Rc4Lane st;
             lane_init(st, S, col, cur.xy);
@@ -1792,7 +1818,7 @@ crypt_stream2_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uin
                                         en < n ? 1u : 0u, payload);
             if (cur.slot != ZRC4_INVALID && cur.len) xy[cur.slot] = lane_xy(st);
         }
-        stream_stamp(sink, 2u + 2u * k_t);
+        stream2_stamp(sink, 2u + 2u * k_t);
         ++k_t;
 
         EntryIn nxt = {0u, ZRC4_INVALID, 0u, 0u};
@@ -1819,7 +1845,7 @@ crypt_stream2_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uin
     }
 #if ZRC4_TIMING
     __builtin_amdgcn_s_waitcnt(0);
-    stream_stamp(sink, 15);
+    stream2_stamp(sink, 15);
 #endif
 }
 #endif  // !ZRC4_XADD16
