@@ -560,6 +560,34 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #define ZRC4_PRIO 1
 #endif
 
+// Line-loop hook at the top of every half (zrc4_line_loop.inc): empty, or --
+// crypt_stream2_kernel with ZRC4_BAL -- progress-balanced issue priority.
+// The wave publishes its progress (blocks done this launch, %[bbase] + sb)
+// in an LDS word, reads the word of the wave sharing its SIMD (the other
+// image's wave), and raises its priority to 3 while it is behind, 1
+// otherwise: the two waves of a SIMD then advance together instead of the
+// older one (or the statically favoured one) finishing ~7 us per group first
+// (profiles/r03/tl_s2.log).  LDS is drained at the hook.
+#define ZRC4_LL_BAL(N)
+#define ZRC4_LL_BAL_ON(N)                                                                        \
+    "s_add_u32 %[bs], %[sb], %[bbase]\n\t"                                                      \
+    "v_mov_b32 %[bv], %[bs]\n\t"                                                                \
+    "ds_write_b32 %[bme], %[bv]\n\t"                                                            \
+    "ds_read_b32 %[bv], %[bpt]\n\t"                                                             \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                  \
+    "v_readfirstlane_b32 %[bt], %[bv]\n\t"                                                      \
+    "s_cmp_lt_u32 %[bs], %[bt]\n\t"                                                             \
+    "s_cbranch_scc1 LL_" #N "BH_%=\n\t"                                                         \
+    "s_setprio 1\n\t"                                                                           \
+    "s_branch LL_" #N "BD_%=\n\t"                                                               \
+    "LL_" #N "BH_%=:\n\t"                                                                       \
+    "s_setprio 3\n\t"                                                                           \
+    "LL_" #N "BD_%=:\n\t"
+
+struct LLBal {
+    uint32_t me, partner, base;   // LDS byte addresses of this wave's / the partner's progress word; blocks done before
+};
+
 #if defined(ZRC4_LL_AB) && ZRC4_LL_AB
 #include "ab/zrc4_line_loop_ab.inc"   // timing-only A/B builds (tools/ab_bench.py --no-check)
 #else
@@ -667,35 +695,49 @@ __device__ __forceinline__ uint32_t hw_id()
 
 // The line loop, halves sb = 0, 2, ... until sb >= wend (wend = wmax: the
 // whole message; wmax rounded down to a multiple of 4, minus 2: all but a
-// final Q half, crypt_last_half_asm).  Returns sb.
+// final Q half, crypt_last_half_asm).  Returns sb.  BAL: the ZRC4_LL_BAL hook.
+#define ZRC4_LL_LINES_BODY                                                                       \
+    "s_mov_b64 %[full], exec\n\t"                                                               \
+    "s_mov_b32 %[sb], 0\n\t"                                                                    \
+    "s_branch LL_PSTART_%=\n\t"                                                                 \
+    "LL_LOOP_%=:\n\t"                                                                           \
+    ZRC4_LL_HALF_P                                                                               \
+    ZRC4_LL_HALF_Q                                                                               \
+    "s_branch LL_LOOP_%=\n\t"                                                                   \
+    "LL_DONE_%=:\n\t"                                                                           \
+    "s_mov_b64 exec, %[full]\n\t"                                                               \
+    "s_nop 1\n\t"                          /* store-data VGPRs: VMEM store -> VALU write hazard */
+#define ZRC4_LL_LINES_OUT                                                                        \
+    [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1), [a0] "+v"(st.a0),        \
+        [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1), [palo] "+v"(palo),              \
+        [pahi] "+v"(pahi), [sb] "=&s"(sb), [s1] "=&s"(s1), [full] "=&s"(full), [msk] "=&s"(msk),       \
+        "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),               \
+        "=&{v[144:151]}"(T)
+#define ZRC4_LL_LINES_IN                                                                         \
+    [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(wend), "{v[136:143]}"(lim), "{v[152:153]}"(sink), \
+        [c100] "s"(0x100u)
+template <bool BAL = false>
 __device__ __forceinline__ uint32_t crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls,
                                                     u32x16 &addr, const u32x8 &lim, u32x2 sink, uint32_t &palo,
-                                                    uint32_t &pahi, uint32_t wend)
+                                                    uint32_t &pahi, uint32_t wend, const LLBal &bal = LLBal{})
 {
     u32x16 X;
     u32x8 T;
     uint32_t b, k0, k1, a1s, sb, s1;
     uint64_t full, msk;
-    asm volatile(
-        "s_mov_b64 %[full], exec\n\t"
-        "s_mov_b32 %[sb], 0\n\t"
-        "s_branch LL_PSTART_%=\n\t"
-        "LL_LOOP_%=:\n\t"
-        ZRC4_LL_HALF_P
-        ZRC4_LL_HALF_Q
-        "s_branch LL_LOOP_%=\n\t"
-        "LL_DONE_%=:\n\t"
-        "s_mov_b64 exec, %[full]\n\t"
-        "s_nop 1\n\t"                          // store-data VGPRs: VMEM store -> VALU write hazard
-        : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1), [a0] "+v"(st.a0),
-          [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
-          [palo] "+v"(palo), [pahi] "+v"(pahi), [sb] "=&s"(sb), [s1] "=&s"(s1),
-          [full] "=&s"(full), [msk] "=&s"(msk),
-          "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
-          "=&{v[144:151]}"(T)
-        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(wend), "{v[136:143]}"(lim), "{v[152:153]}"(sink),
-          [c100] "s"(0x100u)
-        : "memory", "vcc", "scc");
+    if constexpr (BAL) {
+        uint32_t bv, bs, bt;
+#undef ZRC4_LL_BAL
+#define ZRC4_LL_BAL(N) ZRC4_LL_BAL_ON(N)
+        asm volatile(ZRC4_LL_LINES_BODY
+                     : ZRC4_LL_LINES_OUT, [bv] "=&v"(bv), [bs] "=&s"(bs), [bt] "=&s"(bt)
+                     : ZRC4_LL_LINES_IN, [bme] "v"(bal.me), [bpt] "v"(bal.partner), [bbase] "s"(bal.base)
+                     : "memory", "vcc", "scc");
+#undef ZRC4_LL_BAL
+#define ZRC4_LL_BAL(N)
+    } else {
+        asm volatile(ZRC4_LL_LINES_BODY : ZRC4_LL_LINES_OUT : ZRC4_LL_LINES_IN : "memory", "vcc", "scc");
+    }
     return sb;
 }
 
@@ -745,32 +787,47 @@ __device__ __forceinline__ uint32_t crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x
 // nlen / noff: the next group's prefetched entry registers themselves (in
 // flight until the wait; "+v" so the compiler takes them back from here and
 // never copies them before it).
+#define ZRC4_LL_LAST_BODY                                                                        \
+    "s_mov_b64 %[full], exec\n\t"                                                               \
+    ZRC4_NEXT_LINE0                                                                              \
+    ZRC4_LL_HALF_Q                                                                               \
+    "LL_DONE_%=:\n\t"                                                                           \
+    "s_mov_b64 exec, %[full]\n\t"                                                               \
+    "s_waitcnt vmcnt(8)\n\t"             /* the next line 0 (only this half's 8 stores are younger) */ \
+    "s_nop 1\n\t"
+#define ZRC4_LL_LAST_OUT                                                                         \
+    [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1), [a0] "+v"(st.a0),        \
+        [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1), [palo] "+v"(palo),              \
+        [pahi] "+v"(pahi), [sb] "+s"(sb), [s1] "=&s"(s1), [full] "=&s"(full), [msk] "=&s"(msk),        \
+        [h] "=&v"(h), [nb] "=&v"(nb), [nlen] "+v"(nlen), [noff] "+v"(noff), "+{v[40:71]}"(P),          \
+        "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr), "=&{v[144:151]}"(T)
+#define ZRC4_LL_LAST_IN                                                                          \
+    [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(ls.wmax), "{v[136:143]}"(lim),               \
+        "{v[152:153]}"(sink), [nv] "v"(nvalid), [pay] "s"(payload), [c100] "s"(0x100u)
+template <bool BAL = false>
 __device__ __forceinline__ void crypt_last_half_next_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls,
                                                          u32x16 &addr, const u32x8 &lim, u32x2 sink, uint32_t &palo,
                                                          uint32_t &pahi, uint32_t sb, uint32_t &nlen, uint64_t &noff,
-                                                         uint32_t nvalid, const uint8_t *payload)
+                                                         uint32_t nvalid, const uint8_t *payload,
+                                                         const LLBal &bal = LLBal{})
 {
     u32x16 X;
     u32x8 T;
     uint32_t b, k0, k1, a1s, s1, h, nb;
     uint64_t full, msk;
-    asm volatile(
-        "s_mov_b64 %[full], exec\n\t"
-        ZRC4_NEXT_LINE0
-        ZRC4_LL_HALF_Q
-        "LL_DONE_%=:\n\t"
-        "s_mov_b64 exec, %[full]\n\t"
-        "s_waitcnt vmcnt(8)\n\t"             // the next line 0 (only this half's 8 stores are younger)
-        "s_nop 1\n\t"
-        : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1), [a0] "+v"(st.a0),
-          [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
-          [palo] "+v"(palo), [pahi] "+v"(pahi), [sb] "+s"(sb), [s1] "=&s"(s1),
-          [full] "=&s"(full), [msk] "=&s"(msk), [h] "=&v"(h), [nb] "=&v"(nb), [nlen] "+v"(nlen), [noff] "+v"(noff),
-          "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
-          "=&{v[144:151]}"(T)
-        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(ls.wmax), "{v[136:143]}"(lim),
-          "{v[152:153]}"(sink), [nv] "v"(nvalid), [pay] "s"(payload), [c100] "s"(0x100u)
-        : "memory", "vcc", "scc");
+    if constexpr (BAL) {
+        uint32_t bv, bs, bt;
+#undef ZRC4_LL_BAL
+#define ZRC4_LL_BAL(N) ZRC4_LL_BAL_ON(N)
+        asm volatile(ZRC4_LL_LAST_BODY
+                     : ZRC4_LL_LAST_OUT, [bv] "=&v"(bv), [bs] "=&s"(bs), [bt] "=&s"(bt)
+                     : ZRC4_LL_LAST_IN, [bme] "v"(bal.me), [bpt] "v"(bal.partner), [bbase] "s"(bal.base)
+                     : "memory", "vcc", "scc");
+#undef ZRC4_LL_BAL
+#define ZRC4_LL_BAL(N)
+    } else {
+        asm volatile(ZRC4_LL_LAST_BODY : ZRC4_LL_LAST_OUT : ZRC4_LL_LAST_IN : "memory", "vcc", "scc");
+    }
 }
 
 // One group's messages: head bytes, the line loop (line 0 in P, line 1 in
@@ -779,10 +836,11 @@ __device__ __forceinline__ void crypt_last_half_next_asm(Rc4Lane &st, u32x32 &P,
 // next group's line 0 into P before its final half (nlen / noff / nvalid:
 // that group's prefetched entry, crypt_last_half_next_asm); returns true when
 // it did.
+template <bool BAL = false>
 __device__ __forceinline__ bool crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8_t *msg, uint32_t len,
                                                   u32x32 &P, u32x32 &Q, const LineSetup &ls, uint8_t *sinkp,
                                                   bool want_next, uint32_t &nlen, uint64_t &noff, uint32_t nvalid,
-                                                  const uint8_t *payload)
+                                                  const uint8_t *payload, const LLBal &bal = LLBal{})
 {
     const uint32_t head = head_bytes(msg, len);
     for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
@@ -799,10 +857,11 @@ __device__ __forceinline__ bool crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8
         uint32_t palo = (uint32_t)pa, pahi = (uint32_t)(pa >> 32);
         const uint32_t halves = (ls.wmax + 1u) >> 1;
         got = want_next && halves >= 2u && !(halves & 1u);      // wave-uniform
-        const uint32_t sb = crypt_lines_asm(st, P, Q, ls, addr, lim, sk2, palo, pahi,
-                                            got ? 2u * (halves - 1u) : ls.wmax);
+        const uint32_t sb = crypt_lines_asm<BAL>(st, P, Q, ls, addr, lim, sk2, palo, pahi,
+                                                 got ? 2u * (halves - 1u) : ls.wmax, bal);
         if (got)
-            crypt_last_half_next_asm(st, P, Q, ls, addr, lim, sk2, palo, pahi, sb, nlen, noff, nvalid, payload);
+            crypt_last_half_next_asm<BAL>(st, P, Q, ls, addr, lim, sk2, palo, pahi, sb, nlen, noff, nvalid, payload,
+                                          bal);
     }
     uint4 *p = reinterpret_cast<uint4 *>(msg + 64u * ls.nblk);
     uint32_t rem = len & 63u;
@@ -1635,6 +1694,9 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 // Range batches with first_slot % 256 == 0 only (PF).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kStream2Threads = 2u * kGroup;
+#ifndef ZRC4_BAL
+#define ZRC4_BAL 1   // A/B knob: progress-balanced priority between a SIMD's two waves (ZRC4_LL_BAL)
+#endif
 
 // crypt_stream2_kernel (ZRC4_TIMING): lane 0 of EVERY wave stamps event i
 // (0 entry, 1 + 2r / 2 + 2r round r's keystream start / end, 15 exit) as
@@ -1729,7 +1791,7 @@ crypt_stream2_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uin
                      const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
                      uint32_t *__restrict__ err, uint8_t *__restrict__ sink)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kGroupBytes + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kGroupBytes + 64];   // + ZRC4_BAL progress words
     uint8_t *S = smem;
     if (!lds_base_ok(S, err)) return;
     const uint32_t t = threadIdx.x;
@@ -1744,6 +1806,12 @@ crypt_stream2_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uin
     stream2_stamp(sink, 0);
     uint32_t k_t = 0;
     bool p_async = false;
+    // ZRC4_BAL: progress word of (SIMD, image) at LDS 128 KiB + 16; the wave
+    // sharing this wave's SIMD runs the other image
+    const uint32_t simd = (hw_id() >> 4) & 3u;
+    const uint32_t pw = 2u * kGroupBytes + 16u;
+    LLBal bal{pw + 4u * (2u * simd + im), pw + 4u * (2u * simd + (im ^ 1u)), 0u};
+    if (ZRC4_BAL && (t & 63u) == 0u) *reinterpret_cast<volatile uint32_t *>(smem + bal.me) = 0u;
 
     // round r, image im: batch group w = (2r + im) * G + blockIdx.x
     uint32_t w = im * G + blockIdx.x;
@@ -1801,7 +1869,9 @@ crypt_stream2_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uin
         }
 
         // ---- keystream over this image's messages
-#if ZRC4_PRIO == 1
+#if ZRC4_BAL
+        bal.base = 1024u * r;                                    // blocks: monotonic over the rounds
+#elif ZRC4_PRIO == 1
         {
             const uint32_t hw = hw_id();
             if (((hw ^ k_t) & 1u) != 0u)
@@ -1814,8 +1884,8 @@ crypt_stream2_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uin
         if (active) {
             Rc4Lane st;
             lane_init(st, S, col, cur.xy);
-            p_async = crypt_message_dpp(S, st, payload + cur.off, cur.len, P, Q, ls, sk, more, rlen, roff,
-                                        en < n ? 1u : 0u, payload);
+            p_async = crypt_message_dpp<ZRC4_BAL != 0>(S, st, payload + cur.off, cur.len, P, Q, ls, sk, more, rlen,
+                                                       roff, en < n ? 1u : 0u, payload, bal);
             if (cur.slot != ZRC4_INVALID && cur.len) xy[cur.slot] = lane_xy(st);
         }
         stream2_stamp(sink, 2u + 2u * k_t);
