@@ -140,9 +140,6 @@ def half(name: str, cur: int, ab: int = 0) -> str:
     # the previous half's stores (8) and loads (8) -> vmcnt(20).  Halves whose
     # line-after-next does not exist issue no loads, so the LAST half has
     # only 12 younger ops: it waits vmcnt(8) (both blocks) instead.
-    # 0. hook (empty unless the caller defines ZRC4_LL_BAL: crypt_stream2_kernel's
-    #    progress-balanced priority, zrc4_kernels.hpp); LDS is drained here
-    w(f"ZRC4_LL_BAL({name})")
     w(q("s_add_u32 %[s1], %[sb], 2"))
     w(q("s_cmp_ge_u32 %[s1], %[wmax]"))
     w(q(f"s_cbranch_scc0 LL_{name}W_%="))

@@ -54,30 +54,6 @@ def summarise(rt: np.ndarray, clk: np.ndarray, wgs: int, K: int) -> dict:
     return out
 
 
-def summarise_s2(rt: np.ndarray, clk: np.ndarray, wgs: int, K: int) -> dict:
-    """crypt_stream2_kernel: per-wave stamps.  Per round: the waves' keystream
-    times; the wait at the round's end barrier (last wave's end - each wave's
-    end); the per-workgroup spread of ends; plus the kernel-level tail."""
-    r = rt[:wgs * 8].astype(np.float64).reshape(wgs, 8, 16) * 10.0 / 1000.0
-    t0 = r[:, :, 0].min()
-    out = {"workgroups": wgs, "rounds": K, "span_us": round(float(r[:, :, 15].max() - t0), 3),
-           "prologue_us": q(r[:, :, 1] - r[:, :, 0])}
-    for k in range(K):
-        s_, e_ = r[:, :, 1 + 2 * k], r[:, :, 2 + 2 * k]
-        out[f"round{k}"] = {"chain_us": q(e_ - s_),
-                            "barrier_wait_us": q(e_.max(axis=1, keepdims=True) - e_),
-                            "wg_end_spread_us": q(e_.max(axis=1) - e_.min(axis=1)),
-                            "img0_chain_us": q((e_ - s_)[:, :4]), "img1_chain_us": q((e_ - s_)[:, 4:]),
-                            "wg_end_us": q(e_.max(axis=1) - t0)}
-        if k + 1 < K:
-            out[f"round{k}"]["boundary_us"] = q(r[:, :, 3 + 2 * k].min(axis=1) - e_.max(axis=1))
-    end = r[:, :, 15].max(axis=1) - t0
-    out["wg_exit_us"] = q(end)
-    c = clk[:wgs * 8].astype(np.float64).reshape(wgs, 8, 2)
-    out["clock_ghz"] = q((c[:, :, 1] - c[:, :, 0]) / np.maximum(r[:, :, 15] - r[:, :, 0], 1e-9) / 1e3)
-    return out
-
-
 def by_place(rt: np.ndarray, hwid: np.ndarray, wgs: int, K: int) -> dict:
     """Mean keystream time per group (us) of the workgroups, split by XCC, by
     shader engine, and by whether the other workgroup on the CU is an even or
@@ -121,19 +97,14 @@ def main():
                     help="launches before the recorded one: the clock dips for ~30 cfg5 launches and recovers by ~100 (profiles/r02/cfg5_launch_durations.json)")
     ap.add_argument("--footprint-mib", type=int, default=1200)
     ap.add_argument("--build-only", action="store_true")
-    ap.add_argument("--s2", action="store_true",
-                    help="crypt_stream2_kernel (ZRC4_STREAM2): per-wave stamps, 8 waves x 256 workgroups")
     ap.add_argument("--define", action="append", default=[], help="extra -D for the timing build (NAME=V)")
     args = ap.parse_args()
     from zsummerx_amd import build
     defs = {"ZRC4_TIMING": "1"}
-    if args.s2:
-        defs.update(ZRC4_STREAM2="1", ZRC4_XADD16="0")
     for d in args.define:
         k, _, v = d.partition("=")
         defs[k] = v or "1"
-    name = "timing" + ("_s2" if args.s2 else "") + "".join(f"_{k}{v}" for k, v in sorted(defs.items())
-                                                         if k not in ("ZRC4_TIMING", "ZRC4_STREAM2", "ZRC4_XADD16"))
+    name = "timing" + "".join(f"_{k}{v}" for k, v in sorted(defs.items()) if k != "ZRC4_TIMING")
     path = build.build_variant(name, defs)
     if args.build_only:
         print("built", path)
@@ -174,24 +145,6 @@ def main():
         last_event_us = ev0.elapsed_time(ev1) * 1000.0
         sink = C.c_void_p()
         _capi.check(lib.zrc4_debug_sink(h, C.byref(sink)))
-        if args.s2:
-            rt = np.zeros((256 * 8, 16), dtype=np.uint64)
-            clk = np.zeros((256 * 8, 2), dtype=np.uint64)
-            hwid = np.zeros((256 * 8, 2), dtype=np.uint32)
-            for arr, o in ((rt, 0), (clk, 256 << 10), (hwid, 288 << 10)):
-                rc = hip.hipMemcpy(C.c_void_p(arr.ctypes.data), C.c_void_p(sink.value + o), C.c_size_t(arr.nbytes), 2)
-                if rc:
-                    raise SystemExit(f"hipMemcpy failed {rc}")
-            groups = -(-S // 256)
-            wgs = min(-(-groups // 2), 256)
-            rounds = -(-groups // (2 * wgs))
-            out[wl] = summarise_s2(rt, clk, wgs, min(7, rounds))
-            out[wl]["last_launch_event_us"] = round(last_event_us, 2)
-            print(wl, json.dumps(out[wl]), flush=True)
-            lib.zrc4_destroy(h)
-            del keys, pay, off, ln, klen, koff
-            torch.cuda.empty_cache()
-            continue
         rt = np.zeros((512, 16), dtype=np.uint64)
         clk = np.zeros((512, 2), dtype=np.uint64)
         hwid = np.zeros((512, 2), dtype=np.uint32)

@@ -17,12 +17,6 @@
 #ifndef ZRC4_HALF
 #define ZRC4_HALF 1   // A/B knob: 0 runs few-group range batches on whole-group workgroups too
 #endif
-#ifndef ZRC4_STREAM2
-#define ZRC4_STREAM2 0   // A/B knob: aligned range batches above CUs groups run crypt_stream2_kernel
-#endif
-#if ZRC4_STREAM2 && ZRC4_XADD16
-#error "ZRC4_STREAM2 needs ZRC4_XADD16=0 (the x + 1 update must keep bit 16 of the S-box addresses)"
-#endif
 #ifndef ZRC4_WIN_MAX_GROUPS
 #define ZRC4_WIN_MAX_GROUPS 32   // aligned range and grouped batches of at most this many groups run
                                  // 16 lanes per stream (crypt_win_kernel, zrc4_win.hpp); 0 = never
@@ -180,14 +174,6 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
     }
     if (stream_kernel) {
         const uint32_t wgs = std::min(grid, 2u * (uint32_t)c->num_cus);
-#if ZRC4_STREAM2
-        if (mode == zrc4::kRange && (first_slot & 255u) == 0u) {
-            // one 512-thread workgroup per CU, two group images in lockstep
-            const uint32_t g2 = std::min((grid + 1u) / 2u, (uint32_t)c->num_cus);
-            hipLaunchKernelGGL(zrc4::crypt_stream2_kernel, dim3(g2), dim3(zrc4::kStream2Threads), 0, s, c->arena,
-                               c->xy, first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
-        } else
-#endif
         if (mode == zrc4::kRange && (first_slot & 255u) == 0u)
             hipLaunchKernelGGL(zrc4::crypt_stream_kernel<true>, dim3(wgs), blk, 0, s, c->arena, c->xy, ids,
                                first_slot, payload, off, len, n, c->capacity, c->err, c->sink);

@@ -205,9 +205,7 @@ __device__ __forceinline__ void scatter_column(uint8_t *arena, uint32_t slot,
 // ---------------------------------------------------------------------------
 // PRGA (rc4_encryption.h:81-89) on 16-bit LDS addresses.
 //
-// Lane state (all addresses are (index << 8) | col; bytes 2-3 are zero except
-// in crypt_stream2_kernel, whose second image sits at LDS 64 KiB: bit 16 set,
-// kept by every update here and by the asm's byte-1 SDWA writes):
+// Lane state (all addresses are (index << 8) | col, bytes 2-3 zero):
 //   x0 = address of S[x]  where x is the NEXT index to use (stored x + 1)
 //   a0 = S[x]             (already read)
 //   ya = address of S[y]
@@ -246,10 +244,10 @@ __device__ __forceinline__ uint16_t lane_xy(const Rc4Lane &st)
 __device__ __forceinline__ uint32_t prga_step(uint8_t *S, Rc4Lane &st)
 {
     const uint32_t a = st.a0;
-    const uint32_t ya = (st.ya & ~0xFF00u) | ((st.ya + (a << 8)) & 0xFF00u); // y = (u8)(y+a)
+    const uint32_t ya = (st.ya & 0xFFu) | ((st.ya + (a << 8)) & 0xFF00u);  // y = (u8)(y+a)
     const uint32_t b = S[ya];                                                // b = S[y]
     S[ya] = (uint8_t)a;                                                      // S[y] = a
-    const uint32_t xn = (st.x0 & ~0xFF00u) | ((st.x0 + 256u) & 0xFF00u);
+    const uint32_t xn = (st.x0 & 0xFFu) | ((st.x0 + 256u) & 0xFF00u);
     const uint32_t p = S[xn];                                                // next a
     S[st.x0] = (uint8_t)b;                                                   // S[x] = b
     const uint32_t k = S[(((a + b) << 8) & 0xFF00u) | st.col];               // S[(u8)(a+b)]
@@ -560,34 +558,6 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #define ZRC4_PRIO 1
 #endif
 
-// Line-loop hook at the top of every half (zrc4_line_loop.inc): empty, or --
-// crypt_stream2_kernel with ZRC4_BAL -- progress-balanced issue priority.
-// The wave publishes its progress (blocks done this launch, %[bbase] + sb)
-// in an LDS word, reads the word of the wave sharing its SIMD (the other
-// image's wave), and raises its priority to 3 while it is behind, 1
-// otherwise: the two waves of a SIMD then advance together instead of the
-// older one (or the statically favoured one) finishing ~7 us per group first
-// (profiles/r03/tl_s2.log).  LDS is drained at the hook.
-#define ZRC4_LL_BAL(N)
-#define ZRC4_LL_BAL_ON(N)                                                                        \
-    "s_add_u32 %[bs], %[sb], %[bbase]\n\t"                                                      \
-    "v_mov_b32 %[bv], %[bs]\n\t"                                                                \
-    "ds_write_b32 %[bme], %[bv]\n\t"                                                            \
-    "ds_read_b32 %[bv], %[bpt]\n\t"                                                             \
-    "s_waitcnt lgkmcnt(0)\n\t"                                                                  \
-    "v_readfirstlane_b32 %[bt], %[bv]\n\t"                                                      \
-    "s_cmp_lt_u32 %[bs], %[bt]\n\t"                                                             \
-    "s_cbranch_scc1 LL_" #N "BH_%=\n\t"                                                         \
-    "s_setprio 1\n\t"                                                                           \
-    "s_branch LL_" #N "BD_%=\n\t"                                                               \
-    "LL_" #N "BH_%=:\n\t"                                                                       \
-    "s_setprio 3\n\t"                                                                           \
-    "LL_" #N "BD_%=:\n\t"
-
-struct LLBal {
-    uint32_t me, partner, base;   // LDS byte addresses of this wave's / the partner's progress word; blocks done before
-};
-
 #if defined(ZRC4_LL_AB) && ZRC4_LL_AB
 #include "ab/zrc4_line_loop_ab.inc"   // timing-only A/B builds (tools/ab_bench.py --no-check)
 #else
@@ -595,10 +565,8 @@ struct LLBal {
 #endif
 
 constexpr uint32_t kSinkSlot = 256;                 // bytes of sink per thread (128-B line + offsets)
-// crypt_stream2_kernel's 512 threads: slots past the timing build's stamps
-// (stream2_stamp: 256 KiB of per-wave stamps, then clocks and HW ids)
-constexpr uint32_t kSink2Off = ZRC4_TIMING ? (320u << 10) : 0u;
-constexpr uint32_t kSinkBytes = kSink2Off + 2u * kGroup * kSinkSlot;   // per context, shared by all workgroups
+constexpr uint32_t kSinkBytes = kGroup * kSinkSlot  // one 64 KiB sink per context, shared by all workgroups
+                                + (ZRC4_TIMING ? 16384u : 0u);  // + where each timed wave ran / stream clocks and ids
 
 // line = blocks at b0 (16 B x 4) and b1 (16 B x 4)
 __device__ __forceinline__ void preload_line(u32x32 &v, const uint8_t *b0, const uint8_t *b1)
@@ -695,49 +663,35 @@ __device__ __forceinline__ uint32_t hw_id()
 
 // The line loop, halves sb = 0, 2, ... until sb >= wend (wend = wmax: the
 // whole message; wmax rounded down to a multiple of 4, minus 2: all but a
-// final Q half, crypt_last_half_asm).  Returns sb.  BAL: the ZRC4_LL_BAL hook.
-#define ZRC4_LL_LINES_BODY                                                                       \
-    "s_mov_b64 %[full], exec\n\t"                                                               \
-    "s_mov_b32 %[sb], 0\n\t"                                                                    \
-    "s_branch LL_PSTART_%=\n\t"                                                                 \
-    "LL_LOOP_%=:\n\t"                                                                           \
-    ZRC4_LL_HALF_P                                                                               \
-    ZRC4_LL_HALF_Q                                                                               \
-    "s_branch LL_LOOP_%=\n\t"                                                                   \
-    "LL_DONE_%=:\n\t"                                                                           \
-    "s_mov_b64 exec, %[full]\n\t"                                                               \
-    "s_nop 1\n\t"                          /* store-data VGPRs: VMEM store -> VALU write hazard */
-#define ZRC4_LL_LINES_OUT                                                                        \
-    [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1), [a0] "+v"(st.a0),        \
-        [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1), [palo] "+v"(palo),              \
-        [pahi] "+v"(pahi), [sb] "=&s"(sb), [s1] "=&s"(s1), [full] "=&s"(full), [msk] "=&s"(msk),       \
-        "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),               \
-        "=&{v[144:151]}"(T)
-#define ZRC4_LL_LINES_IN                                                                         \
-    [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(wend), "{v[136:143]}"(lim), "{v[152:153]}"(sink), \
-        [c100] "s"(0x100u)
-template <bool BAL = false>
+// final Q half, crypt_last_half_asm).  Returns sb.
 __device__ __forceinline__ uint32_t crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls,
                                                     u32x16 &addr, const u32x8 &lim, u32x2 sink, uint32_t &palo,
-                                                    uint32_t &pahi, uint32_t wend, const LLBal &bal = LLBal{})
+                                                    uint32_t &pahi, uint32_t wend)
 {
     u32x16 X;
     u32x8 T;
     uint32_t b, k0, k1, a1s, sb, s1;
     uint64_t full, msk;
-    if constexpr (BAL) {
-        uint32_t bv, bs, bt;
-#undef ZRC4_LL_BAL
-#define ZRC4_LL_BAL(N) ZRC4_LL_BAL_ON(N)
-        asm volatile(ZRC4_LL_LINES_BODY
-                     : ZRC4_LL_LINES_OUT, [bv] "=&v"(bv), [bs] "=&s"(bs), [bt] "=&s"(bt)
-                     : ZRC4_LL_LINES_IN, [bme] "v"(bal.me), [bpt] "v"(bal.partner), [bbase] "s"(bal.base)
-                     : "memory", "vcc", "scc");
-#undef ZRC4_LL_BAL
-#define ZRC4_LL_BAL(N)
-    } else {
-        asm volatile(ZRC4_LL_LINES_BODY : ZRC4_LL_LINES_OUT : ZRC4_LL_LINES_IN : "memory", "vcc", "scc");
-    }
+    asm volatile(
+        "s_mov_b64 %[full], exec\n\t"
+        "s_mov_b32 %[sb], 0\n\t"
+        "s_branch LL_PSTART_%=\n\t"
+        "LL_LOOP_%=:\n\t"
+        ZRC4_LL_HALF_P
+        ZRC4_LL_HALF_Q
+        "s_branch LL_LOOP_%=\n\t"
+        "LL_DONE_%=:\n\t"
+        "s_mov_b64 exec, %[full]\n\t"
+        "s_nop 1\n\t"                          // store-data VGPRs: VMEM store -> VALU write hazard
+        : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1), [a0] "+v"(st.a0),
+          [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
+          [palo] "+v"(palo), [pahi] "+v"(pahi), [sb] "=&s"(sb), [s1] "=&s"(s1),
+          [full] "=&s"(full), [msk] "=&s"(msk),
+          "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
+          "=&{v[144:151]}"(T)
+        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(wend), "{v[136:143]}"(lim), "{v[152:153]}"(sink),
+          [c100] "s"(0x100u)
+        : "memory", "vcc", "scc");
     return sb;
 }
 
@@ -787,47 +741,32 @@ __device__ __forceinline__ uint32_t crypt_lines_asm(Rc4Lane &st, u32x32 &P, u32x
 // nlen / noff: the next group's prefetched entry registers themselves (in
 // flight until the wait; "+v" so the compiler takes them back from here and
 // never copies them before it).
-#define ZRC4_LL_LAST_BODY                                                                        \
-    "s_mov_b64 %[full], exec\n\t"                                                               \
-    ZRC4_NEXT_LINE0                                                                              \
-    ZRC4_LL_HALF_Q                                                                               \
-    "LL_DONE_%=:\n\t"                                                                           \
-    "s_mov_b64 exec, %[full]\n\t"                                                               \
-    "s_waitcnt vmcnt(8)\n\t"             /* the next line 0 (only this half's 8 stores are younger) */ \
-    "s_nop 1\n\t"
-#define ZRC4_LL_LAST_OUT                                                                         \
-    [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1), [a0] "+v"(st.a0),        \
-        [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1), [palo] "+v"(palo),              \
-        [pahi] "+v"(pahi), [sb] "+s"(sb), [s1] "=&s"(s1), [full] "=&s"(full), [msk] "=&s"(msk),        \
-        [h] "=&v"(h), [nb] "=&v"(nb), [nlen] "+v"(nlen), [noff] "+v"(noff), "+{v[40:71]}"(P),          \
-        "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr), "=&{v[144:151]}"(T)
-#define ZRC4_LL_LAST_IN                                                                          \
-    [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(ls.wmax), "{v[136:143]}"(lim),               \
-        "{v[152:153]}"(sink), [nv] "v"(nvalid), [pay] "s"(payload), [c100] "s"(0x100u)
-template <bool BAL = false>
 __device__ __forceinline__ void crypt_last_half_next_asm(Rc4Lane &st, u32x32 &P, u32x32 &Q, const LineSetup &ls,
                                                          u32x16 &addr, const u32x8 &lim, u32x2 sink, uint32_t &palo,
                                                          uint32_t &pahi, uint32_t sb, uint32_t &nlen, uint64_t &noff,
-                                                         uint32_t nvalid, const uint8_t *payload,
-                                                         const LLBal &bal = LLBal{})
+                                                         uint32_t nvalid, const uint8_t *payload)
 {
     u32x16 X;
     u32x8 T;
     uint32_t b, k0, k1, a1s, s1, h, nb;
     uint64_t full, msk;
-    if constexpr (BAL) {
-        uint32_t bv, bs, bt;
-#undef ZRC4_LL_BAL
-#define ZRC4_LL_BAL(N) ZRC4_LL_BAL_ON(N)
-        asm volatile(ZRC4_LL_LAST_BODY
-                     : ZRC4_LL_LAST_OUT, [bv] "=&v"(bv), [bs] "=&s"(bs), [bt] "=&s"(bt)
-                     : ZRC4_LL_LAST_IN, [bme] "v"(bal.me), [bpt] "v"(bal.partner), [bbase] "s"(bal.base)
-                     : "memory", "vcc", "scc");
-#undef ZRC4_LL_BAL
-#define ZRC4_LL_BAL(N)
-    } else {
-        asm volatile(ZRC4_LL_LAST_BODY : ZRC4_LL_LAST_OUT : ZRC4_LL_LAST_IN : "memory", "vcc", "scc");
-    }
+    asm volatile(
+        "s_mov_b64 %[full], exec\n\t"
+        ZRC4_NEXT_LINE0
+        ZRC4_LL_HALF_Q
+        "LL_DONE_%=:\n\t"
+        "s_mov_b64 exec, %[full]\n\t"
+        "s_waitcnt vmcnt(8)\n\t"             // the next line 0 (only this half's 8 stores are younger)
+        "s_nop 1\n\t"
+        : [ya] "+v"(st.ya), [ta] "+v"(st.ta), [x0] "+v"(st.x0), [x1] "+v"(st.x1), [a0] "+v"(st.a0),
+          [a1] "=&v"(a1s), [b] "=&v"(b), [k0] "=&v"(k0), [k1] "=&v"(k1),
+          [palo] "+v"(palo), [pahi] "+v"(pahi), [sb] "+s"(sb), [s1] "=&s"(s1),
+          [full] "=&s"(full), [msk] "=&s"(msk), [h] "=&v"(h), [nb] "=&v"(nb), [nlen] "+v"(nlen), [noff] "+v"(noff),
+          "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[104:119]}"(X), "+{v[120:135]}"(addr),
+          "=&{v[144:151]}"(T)
+        : [nblk] "v"(ls.nblk), [wmax] "s"(ls.wmax), [wend] "s"(ls.wmax), "{v[136:143]}"(lim),
+          "{v[152:153]}"(sink), [nv] "v"(nvalid), [pay] "s"(payload), [c100] "s"(0x100u)
+        : "memory", "vcc", "scc");
 }
 
 // One group's messages: head bytes, the line loop (line 0 in P, line 1 in
@@ -836,11 +775,10 @@ __device__ __forceinline__ void crypt_last_half_next_asm(Rc4Lane &st, u32x32 &P,
 // next group's line 0 into P before its final half (nlen / noff / nvalid:
 // that group's prefetched entry, crypt_last_half_next_asm); returns true when
 // it did.
-template <bool BAL = false>
 __device__ __forceinline__ bool crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8_t *msg, uint32_t len,
                                                   u32x32 &P, u32x32 &Q, const LineSetup &ls, uint8_t *sinkp,
                                                   bool want_next, uint32_t &nlen, uint64_t &noff, uint32_t nvalid,
-                                                  const uint8_t *payload, const LLBal &bal = LLBal{})
+                                                  const uint8_t *payload)
 {
     const uint32_t head = head_bytes(msg, len);
     for (uint32_t i = 0; i < head; ++i) msg[i] ^= (uint8_t)prga_step(S, st);
@@ -857,11 +795,10 @@ __device__ __forceinline__ bool crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8
         uint32_t palo = (uint32_t)pa, pahi = (uint32_t)(pa >> 32);
         const uint32_t halves = (ls.wmax + 1u) >> 1;
         got = want_next && halves >= 2u && !(halves & 1u);      // wave-uniform
-        const uint32_t sb = crypt_lines_asm<BAL>(st, P, Q, ls, addr, lim, sk2, palo, pahi,
-                                                 got ? 2u * (halves - 1u) : ls.wmax, bal);
+        const uint32_t sb = crypt_lines_asm(st, P, Q, ls, addr, lim, sk2, palo, pahi,
+                                            got ? 2u * (halves - 1u) : ls.wmax);
         if (got)
-            crypt_last_half_next_asm<BAL>(st, P, Q, ls, addr, lim, sk2, palo, pahi, sb, nlen, noff, nvalid, payload,
-                                          bal);
+            crypt_last_half_next_asm(st, P, Q, ls, addr, lim, sk2, palo, pahi, sb, nlen, noff, nvalid, payload);
     }
     uint4 *p = reinterpret_cast<uint4 *>(msg + 64u * ls.nblk);
     uint32_t rem = len & 63u;
@@ -1676,249 +1613,6 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     stream_stamp(sink, 15);
 #endif
 }
-
-// ---------------------------------------------------------------------------
-// crypt_stream2_kernel (ZRC4_STREAM2): the throughput kernel as ONE 512-thread
-// workgroup per CU holding TWO group images -- image 0 at LDS 0 for waves 0-3,
-// image 1 at LDS 64 KiB for waves 4-7 (bit 16 of every S-box address register;
-// the asm's byte-1 SDWA updates keep it, so ZRC4_XADD16 must be 0: a 16-bit
-// VOP2 add zeroes bits 16-31 on gfx9).  Same per-thread work as
-// crypt_stream_kernel (prefetched image and entries, line loop, copy-out),
-// but the two images advance in lockstep rounds: round r runs groups
-// (2r + i) * grid + wg, i = image, and every barrier is the whole CU's.
-// Why: with two 256-thread workgroups per CU, one workgroup ran ahead of the
-// other (the older waves win the SIMDs' issue arbitration; 2.9 us per group
-// between the two of a CU against 0.9 us of spread between CU means,
-// profiles/r02/stream_tl_pairs.log) and the last one finished ~27 us after
-// the median; here a CU's 8 waves meet at every group boundary.
-// Range batches with first_slot % 256 == 0 only (PF).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kStream2Threads = 2u * kGroup;
-#ifndef ZRC4_BAL
-#define ZRC4_BAL 1   // A/B knob: progress-balanced priority between a SIMD's two waves (ZRC4_LL_BAL)
-#endif
-
-// crypt_stream2_kernel (ZRC4_TIMING): lane 0 of EVERY wave stamps event i
-// (0 entry, 1 + 2r / 2 + 2r round r's keystream start / end, 15 exit) as
-// s_memrealtime into sink[(wg * 8 + wave) * 16 + i] (256 workgroups); entry /
-// exit shader clocks at sink + 256 KiB, HW_ID / XCC_ID at sink + 288 KiB
-// (tools/stream_timeline.py --s2).
-__device__ __forceinline__ void stream2_stamp(uint8_t *sink, uint32_t i)
-{
-#if ZRC4_TIMING
-    const uint32_t wave = threadIdx.x >> 6, slot = blockIdx.x * 8u + wave;
-    if ((threadIdx.x & 63u) == 0u && blockIdx.x < 256u && i < 16u) {
-        reinterpret_cast<uint64_t *>(sink)[slot * 16u + i] = __builtin_amdgcn_s_memrealtime();
-        if (i == 0u || i == 15u)
-            reinterpret_cast<uint64_t *>(sink + (256u << 10))[slot * 2u + (i ? 1u : 0u)] = __builtin_amdgcn_s_memtime();
-        if (i == 0u) {
-            uint32_t hw, xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
-                         : "=s"(hw), "=s"(xcc));
-            uint32_t *o = reinterpret_cast<uint32_t *>(sink + (288u << 10)) + slot * 2u;
-            o[0] = hw;
-            o[1] = xcc;
-        }
-    }
-#endif
-}
-
-__device__ __forceinline__ void lds_to_image2_asm(uint8_t *img, uint32_t tid, uint32_t lbase)
-{
-    u32x32 d0, d1;
-    uint32_t vo, vl;
-    asm volatile(
-        "v_lshlrev_b32 %[vo], 4, %[t]\n\t"
-        "v_or_b32 %[vl], %[vo], %[lb]\n\t"
-        "ds_read_b128 v[72:75], %[vl]\n\t"
-        "ds_read_b128 v[76:79], %[vl] offset:4096\n\t"
-        "ds_read_b128 v[80:83], %[vl] offset:8192\n\t"
-        "ds_read_b128 v[84:87], %[vl] offset:12288\n\t"
-        "ds_read_b128 v[88:91], %[vl] offset:16384\n\t"
-        "ds_read_b128 v[92:95], %[vl] offset:20480\n\t"
-        "ds_read_b128 v[96:99], %[vl] offset:24576\n\t"
-        "ds_read_b128 v[100:103], %[vl] offset:28672\n\t"
-        "ds_read_b128 v[104:107], %[vl] offset:32768\n\t"
-        "ds_read_b128 v[108:111], %[vl] offset:36864\n\t"
-        "ds_read_b128 v[112:115], %[vl] offset:40960\n\t"
-        "ds_read_b128 v[116:119], %[vl] offset:45056\n\t"
-        "ds_read_b128 v[120:123], %[vl] offset:49152\n\t"
-        "ds_read_b128 v[124:127], %[vl] offset:53248\n\t"
-        "ds_read_b128 v[128:131], %[vl] offset:57344\n\t"
-        "ds_read_b128 v[132:135], %[vl] offset:61440\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "global_store_dwordx4 %[vo], v[72:75], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[76:79], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[80:83], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[84:87], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[88:91], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[92:95], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[96:99], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[100:103], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[104:107], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[108:111], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[112:115], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[116:119], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[120:123], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[124:127], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[128:131], %[img]\n\t"
-        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
-        "global_store_dwordx4 %[vo], v[132:135], %[img]\n\t"
-        "s_nop 1\n\t"                          // store-data VGPRs: VMEM store -> VALU write hazard
-        : "=&{v[72:103]}"(d0), "=&{v[104:135]}"(d1), [vo] "=&v"(vo), [vl] "=&v"(vl)
-        : [t] "v"(tid), [img] "s"(img), [lb] "v"(lbase)
-        : "memory");
-}
-
-#if !ZRC4_XADD16
-__global__ void __launch_bounds__(kStream2Threads, 1)
-crypt_stream2_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, uint32_t first_slot,
-                     uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
-                     const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
-                     uint32_t *__restrict__ err, uint8_t *__restrict__ sink)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kGroupBytes + 64];   // + ZRC4_BAL progress words
-    uint8_t *S = smem;
-    if (!lds_base_ok(S, err)) return;
-    const uint32_t t = threadIdx.x;
-    const uint32_t im = __builtin_amdgcn_readfirstlane(t >> 8);       // image of this wave
-    const uint32_t j = t & 255u;                                       // group lane
-    const uint32_t lb = im << 16;                                      // LDS base of the image
-    const uint32_t col = col_of(j) | lb;
-    const uint32_t nwg = (n + kGroup - 1) / kGroup;
-    const uint32_t G = gridDim.x;
-    uint8_t *sk = sink + kSink2Off + (size_t)t * kSinkSlot;
-    const uint32_t g0 = first_slot >> 8;
-    stream2_stamp(sink, 0);
-    uint32_t k_t = 0;
-    bool p_async = false;
-    // ZRC4_BAL: progress word of (SIMD, image) at LDS 128 KiB + 16; the wave
-    // sharing this wave's SIMD runs the other image
-    const uint32_t simd = (hw_id() >> 4) & 3u;
-    const uint32_t pw = 2u * kGroupBytes + 16u;
-    LLBal bal{pw + 4u * (2u * simd + im), pw + 4u * (2u * simd + (im ^ 1u)), 0u};
-    if (ZRC4_BAL && (t & 63u) == 0u) *reinterpret_cast<volatile uint32_t *>(smem + bal.me) = 0u;
-
-    // round r, image im: batch group w = (2r + im) * G + blockIdx.x
-    uint32_t w = im * G + blockIdx.x;
-    bool active = w < nwg;
-    EntryIn cur = {0u, ZRC4_INVALID, 0u, 0u};
-    u32x32 ilo, ihi;
-    if (active) {
-        load_entry(cur, w, j, nullptr, first_slot, off, len, n, capacity, err, xy);
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(arena + (size_t)(g0 + w) * kGroupBytes);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const u32x4 a = src[i * 256 + j], b = src[(i + 8) * 256 + j];
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                ilo[4 * i + d] = a[d];
-                ihi[4 * i + d] = b[d];
-            }
-        }
-    }
-    LineSetup ls;
-    line_setup(ls, payload + cur.off, cur.len);
-    u32x32 P, Q = {};
-    preload_line0(P, ls, sk);
-    asm volatile("" : "+v"(cur.len), "+v"(cur.off), "+v"(cur.xy), "+{v[40:71]}"(P),
-                 "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi));
-
-    for (uint32_t r = 0;; ++r) {
-        // ---- this round's S-boxes into LDS (both images, one barrier)
-        if (active) {
-            asm volatile("s_waitcnt vmcnt(24)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
-            u32x4 *dst = reinterpret_cast<u32x4 *>(S + lb);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                dst[i * 256 + j] = u32x4{ilo[4 * i], ilo[4 * i + 1], ilo[4 * i + 2], ilo[4 * i + 3]};
-                dst[(i + 8) * 256 + j] = u32x4{ihi[4 * i], ihi[4 * i + 1], ihi[4 * i + 2], ihi[4 * i + 3]};
-            }
-        }
-        __syncthreads();
-
-        // ---- next round's entries and image for this wave's image, in flight during the keystream
-        const uint32_t wn = w + 2u * G;
-        const bool more = wn < nwg;                              // wave-uniform
-        const bool more_any = (2u * (r + 1u)) * G + blockIdx.x < nwg;   // image 0 next round: workgroup-uniform
-        uint32_t rlen = 0, rxy = 0;
-        uint64_t roff = 0;
-        uint32_t en = 0;
-        asm volatile("" : "+{v[40:71]}"(P));
-        p_async = false;
-        if (active && ls.wmax > 2u) issue_line1_asm(Q, ls, sk);
-        if (active && more) {
-            en = wn * kGroup + j;
-            const uint32_t ec = en < n ? en : n - 1u;
-            prefetch_group(P, Q, ilo, ihi, rlen, roff, rxy, len + ec, off + ec, xy + first_slot + ec,
-                           arena + (size_t)(g0 + wn) * kGroupBytes, j);
-        }
-
-        // ---- keystream over this image's messages
-#if ZRC4_BAL
-        bal.base = 1024u * r;                                    // blocks: monotonic over the rounds
-#elif ZRC4_PRIO == 1
-        {
-            const uint32_t hw = hw_id();
-            if (((hw ^ k_t) & 1u) != 0u)
-                __builtin_amdgcn_s_setprio(2);
-            else
-                __builtin_amdgcn_s_setprio(1);
-        }
-#endif
-        stream2_stamp(sink, 1u + 2u * k_t);
-        if (active) {
-            Rc4Lane st;
-            lane_init(st, S, col, cur.xy);
-            p_async = crypt_message_dpp<ZRC4_BAL != 0>(S, st, payload + cur.off, cur.len, P, Q, ls, sk, more, rlen,
-                                                       roff, en < n ? 1u : 0u, payload, bal);
-            if (cur.slot != ZRC4_INVALID && cur.len) xy[cur.slot] = lane_xy(st);
-        }
-        stream2_stamp(sink, 2u + 2u * k_t);
-        ++k_t;
-
-        EntryIn nxt = {0u, ZRC4_INVALID, 0u, 0u};
-        if (active && more) {
-            if (!p_async)
-                asm volatile("s_waitcnt vmcnt(16)" : "+v"(rlen), "+v"(roff), "+v"(rxy) :: "memory");
-            const bool v = en < n;
-            nxt.len = v ? rlen : 0u;
-            nxt.off = v ? roff : 0u;
-            nxt.slot = v ? first_slot + en : ZRC4_INVALID;
-            nxt.xy = v ? rxy : 0u;
-            line_setup(ls, payload + nxt.off, nxt.len);
-            if (!p_async) preload_line0(P, ls, sk);
-        }
-
-        // ---- this round's state back to HBM
-        __syncthreads();
-        if (active) lds_to_image2_asm(arena + (size_t)(g0 + w) * kGroupBytes, j, lb);
-        if (!more_any) break;
-        __syncthreads();      // every wave has read its image out of LDS before the next fill
-        active = active && more;
-        cur = nxt;
-        w = wn;
-    }
-#if ZRC4_TIMING
-    __builtin_amdgcn_s_waitcnt(0);
-    stream2_stamp(sink, 15);
-#endif
-}
-#endif  // !ZRC4_XADD16
 
 // ---------------------------------------------------------------------------
 // ksa_kernel: batched RC4Encryption::makeSBox (rc4_encryption.h:46-72).
