@@ -116,6 +116,43 @@ int zrc4_xor_ring(zrc4_ctx *, uint8_t *ring, uint32_t cap, const uint32_t *rid, 
     }
     return ZRC4_OK;
 }
+// Keystream reservoirs (zrc4_ks_*) as their observable semantics: the C++
+// mirror (include/zsummerx_amd/rc4_encryption.h) over this emulation crypts
+// every call straight on the oracle state (no rings to emulate: a reservoir
+// changes when keystream is made, never which bytes come out).
+struct zrc4_ks {
+    zrc4_ctx *c;
+};
+int zrc4_ks_create(zrc4_ctx *c, uint32_t, zrc4_ks **out)
+{
+    *out = new zrc4_ks{c};
+    return ZRC4_OK;
+}
+int zrc4_ks_destroy(zrc4_ks *k)
+{
+    delete k;
+    return ZRC4_OK;
+}
+int zrc4_ks_crypt(zrc4_ks *k, const uint32_t *ids, uint8_t *const *data, const uint32_t *len, uint32_t n)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        if (ids[i] >= k->c->st.size()) return ZRC4_ERR_SLOT_RANGE;
+        oracle_encryption(&k->c->st[ids[i]], data[i], (long)len[i]);
+    }
+    return ZRC4_OK;
+}
+int zrc4_ks_make_sbox(zrc4_ks *k, uint32_t id, const uint8_t *key, size_t keylen)
+{
+    if (id >= k->c->st.size()) return ZRC4_ERR_SLOT_RANGE;
+    oracle_make_sbox(&k->c->st[id], key, keylen);
+    return ZRC4_OK;
+}
+int zrc4_ks_copy(zrc4_ks *dk, uint32_t dst, zrc4_ks *sk, uint32_t src)
+{
+    if (dst >= dk->c->st.size() || src >= sk->c->st.size()) return ZRC4_ERR_SLOT_RANGE;
+    dk->c->st[dst] = sk->c->st[src];
+    return ZRC4_OK;
+}
 int zrc4_sync(zrc4_ctx *, void *) { return ZRC4_OK; }
 int zrc4_poll_faults(zrc4_ctx *) { return ZRC4_OK; }
 const char *zrc4_strerror(int) { return "emulated zrc4"; }

@@ -1017,6 +1017,12 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         constexpr uint32_t kMul = ZRC4_WPERM + 0u;
         if (gridDim.x % kMul != 0u) wg = (blockIdx.x * kMul) % gridDim.x;
     }
+#if defined(ZRC4_STAGGER) && ZRC4_STAGGER
+    // A/B diagnostic (cfg3 write traffic): workgroup start spread over
+    // 0..7 x ZRC4_STAGGER x 64 cycles, as a grouped launch's longer prologue spreads it
+    if constexpr (MODE == kRange && !HALF)
+        for (uint32_t i = 0; i < (blockIdx.x & 7u); ++i) __builtin_amdgcn_s_sleep(ZRC4_STAGGER);
+#endif
     const uint32_t e = wg * kLanes + tid;                // batch entry of this thread
     const bool valid = e < n;
     const uint32_t h = HALF ? (blockIdx.x & 1u) : 0u;    // half of the group (HALF)
