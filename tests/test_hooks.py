@@ -59,6 +59,34 @@ def test_reservoir_parallel_xor_emulated(tools, threads):
     assert out["hooks"]["xor_threads"] == threads and out["hooks"]["ring_bytes"] > 0
 
 
+@pytest.mark.parametrize("seed", [1, 3])
+def test_adaptive_mode_switches_emulated(tools, seed):
+    """Adaptive hooks (r03): with the switch point near this run's ~166 KB per
+    call the moving average crosses it both ways -- refills stop (spans drain
+    their rings, then go to the device as tails) and resume -- and every byte
+    still matches the oracle."""
+    import os
+    env = dict(os.environ, ZSX_RC4_DIRECT_BYTES="170000")
+    out = run(tools / "hooks_check_emu", "device", 48, 150, seed, env=env)
+    h = out["hooks"]
+    assert 0 < h["direct_calls"] < 150, h
+    assert h["refill_launches"] > 0 and h["ring_bytes"] > 0 and h["tail_bytes"] > 0, h
+
+
+def test_adaptive_mode_all_direct_emulated(tools):
+    import os
+    env = dict(os.environ, ZSX_RC4_DIRECT_BYTES="1")
+    out = run(tools / "hooks_check_emu", "device", 48, 150, 2, env=env)
+    assert out["hooks"]["direct_calls"] == 150 and out["hooks"]["ring_bytes"] == 0, out["hooks"]
+
+
+def test_adaptive_mode_off_emulated(tools):
+    import os
+    env = dict(os.environ, ZSX_RC4_DIRECT_BYTES="0")
+    out = run(tools / "hooks_check_emu", "device", 48, 150, 2, env=env)
+    assert out["hooks"]["direct_calls"] == 0 and out["hooks"]["direct_bytes"] == 0, out["hooks"]
+
+
 def test_direct_host_logic_emulated(tools):
     run(tools / "hooks_check_emu", "direct", 16, 40, 9)
 
@@ -83,6 +111,15 @@ def test_device_hooks_parallel_xor(tools):
 def test_device_hooks_small_ring(tools):
     out = run(tools / "hooks_check", "device", 96, 150, 11, 1000)
     assert out["hooks"]["tail_bytes"] > 0 and out["hooks"]["ring_bytes"] > 0
+
+
+@pytest.mark.gpu
+def test_device_hooks_adaptive_mode_switches(tools):
+    import os
+    env = dict(os.environ, ZSX_RC4_DIRECT_BYTES="170000")
+    out = run(tools / "hooks_check", "device", 48, 150, 3, env=env)
+    h = out["hooks"]
+    assert 0 < h["direct_calls"] < 150 and h["refill_launches"] > 0 and h["tail_bytes"] > 0, h
 
 
 @pytest.mark.gpu

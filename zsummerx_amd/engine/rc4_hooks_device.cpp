@@ -430,13 +430,14 @@ public:
 
     std::string stats() const override
     {
-        char b[512];
+        char b[768];
         std::snprintf(b, sizeof b,
                       "{\"ring_bytes\": %llu, \"tail_bytes\": %llu, \"tail_launches\": %llu, "
                       "\"refill_bytes\": %llu, \"refill_launches\": %llu, \"refill_waits\": %llu, "
-                      "\"ring_cap\": %u, \"refill_chunk\": %u, \"device_framed\": %llu, \"xor_threads\": %u}",
+                      "\"ring_cap\": %u, \"refill_chunk\": %u, \"device_framed\": %llu, \"xor_threads\": %u, "
+                      "\"direct_calls\": %llu, \"direct_bytes\": %llu}",
                       ringBytes_, tailBytes_, tailLaunches_, refillBytes_, refillLaunches_, refillWaits_, ringCap_,
-                      refillChunk_, framed_, xor_.threads());
+                      refillChunk_, framed_, xor_.threads(), directCalls_, (unsigned long long)directBytes_);
         return b;
     }
 
@@ -482,8 +483,31 @@ private:
         return runTail(es_);
     }
 
+    // Adaptive mode (r03).  The reservoir wins while an iteration is small
+    // (a host XOR, no GPU round trip on the latency path); with megabytes per
+    // iteration the host XOR of every span dominates and one grouped launch
+    // over the spans in place (zero-copy pinned blocks) wins: 2048 x 2
+    // sessions (~4 MB per call) 134k vs 172k echo/s, 512 x 4 (~1.8 MB) 210k vs
+    // 223k, while 512 x 1 (~0.45 MB) runs 228k vs 212k the other way
+    // (profiles/r02/frame_loopback_win_v17.jsonl).  So the hooks follow a
+    // moving average of the bytes per call: at or above $ZSX_RC4_DIRECT_BYTES
+    // (default 1 MiB; 0 = never) they stop refilling -- each slot drains
+    // what its ring holds, then its spans go to the device as tails, which
+    // is exactly the direct mode's launch -- and below half of it refills
+    // resume.  The keystream order is the same either way.
+    void updateMode(const Rc4Span *spans, uint32_t n)
+    {
+        uint64_t bytes = 0;
+        for (uint32_t i = 0; i < n; ++i) bytes += spans[i].len;
+        emaBytes_ = emaBytes_ == 0.0 ? (double)bytes : 0.875 * emaBytes_ + 0.125 * (double)bytes;
+        if (directBytes_ && !direct_ && emaBytes_ >= (double)directBytes_) direct_ = true;
+        else if (direct_ && emaBytes_ < 0.5 * (double)directBytes_) direct_ = false;
+        if (direct_) ++directCalls_;
+    }
+
     int cryptReservoir(const Rc4Span *spans, uint32_t n)
     {
+        updateMode(spans, n);
         int rc = pollRefills(false);
         if (rc != ZRC4_OK) return rc;
         // A slot short of committed keystream while refills are queued: wait
@@ -530,7 +554,7 @@ private:
                 L.gen = L.pend = L.use;
                 tailBytes_ += sp.len - have;
             }
-            if (!hungryMark_[sp.slot]) {
+            if (!direct_ && !hungryMark_[sp.slot]) {
                 hungryMark_[sp.slot] = 1;
                 hungry_.push_back(sp.slot);
             }
@@ -540,7 +564,7 @@ private:
             if ((rc = drainRefills()) != ZRC4_OK) return rc;     // slot state must be quiet
             if ((rc = runTail(es_)) != ZRC4_OK) return rc;
         }
-        while (inFlight_ < refillDepth_) {
+        while (!direct_ && inFlight_ < refillDepth_) {
             const uint32_t before = inFlight_;
             if ((rc = launchRefill()) != ZRC4_OK) return rc;
             if (inFlight_ == before) break;
@@ -724,6 +748,12 @@ private:
     static constexpr uint32_t kRefillDepth = 2;
     const uint32_t refillDepth_ = std::getenv("ZSX_REFILL_DEPTH") ? std::max(1, std::min(2, std::atoi(std::getenv("ZSX_REFILL_DEPTH")))) : kRefillDepth;
     static constexpr int ZRC4_ERR_NOT_READY_ = 1;   // internal: oldest refill still running
+    const uint64_t directBytes_ = std::getenv("ZSX_RC4_DIRECT_BYTES")
+                                     ? std::strtoull(std::getenv("ZSX_RC4_DIRECT_BYTES"), nullptr, 10)
+                                     : (1ull << 20);
+    double emaBytes_ = 0.0;
+    bool direct_ = false;
+    unsigned long long directCalls_ = 0;
     const bool debugNoRefill_ = std::getenv("ZSX_RESERVOIR_NO_REFILL") != nullptr;   // test knobs
     const bool debugSyncRefill_ = std::getenv("ZSX_RESERVOIR_SYNC_REFILL") != nullptr;
 
