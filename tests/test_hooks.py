@@ -100,9 +100,19 @@ def test_device_hooks_vs_oracle(tools, mode, sessions, rounds, seed):
 
 
 @pytest.mark.gpu
+def test_device_hooks_reservoir_at_scale(tools):
+    """2 048 sessions with the adaptive switch off: the reservoir path itself
+    at a size where the default hooks would run direct launches."""
+    import os
+    out = run(tools / "hooks_check", "device", 2048, 50, 3, env=dict(os.environ, ZSX_RC4_DIRECT_BYTES="0"))
+    assert out["hooks"]["ring_bytes"] > 0 and out["hooks"]["direct_calls"] == 0, out["hooks"]
+
+
+@pytest.mark.gpu
 def test_device_hooks_parallel_xor(tools):
     import os
-    env = dict(os.environ, ZSX_XOR_THREADS="4", ZSX_XOR_MIN_BYTES="0")
+    # 512 sessions a call is past the adaptive switch point: the reservoir alone here
+    env = dict(os.environ, ZSX_XOR_THREADS="4", ZSX_XOR_MIN_BYTES="0", ZSX_RC4_DIRECT_BYTES="0")
     out = run(tools / "hooks_check", "device", 512, 60, 17, env=env)
     assert out["hooks"]["xor_threads"] == 4 and out["hooks"]["ring_bytes"] > 0
 
