@@ -17,7 +17,7 @@ timeout -k 10 400 python -u -m pytest tests/test_frame.py tests/test_hooks.py -m
 rc=$?; tail -3 $OUT/frame_tests.log; echo "[frame-tests] rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 : > $OUT/frame_loopback.jsonl
-for cfg in "2 1" "2 4" "64 1" "64 4" "512 1" "512 4" "2048 2"; do
+for cfg in ${CFGS:-"2 1" "2 4" "64 1" "64 4" "512 1" "512 4" "2048 2"}; do
   set -- $cfg
   for mode in ${MODES:-adaptive reservoir direct adaptive reservoir direct adaptive reservoir direct reference off}; do
     case $mode in
