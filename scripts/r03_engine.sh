@@ -18,7 +18,7 @@ rc=$?; tail -3 $OUT/frame_tests.log; echo "[frame-tests] rc=$rc"; [ $rc -eq 0 ] 
 fi
 : > $OUT/frame_loopback.jsonl
 for cfg in ${CFGS:-"2 1" "2 4" "64 1" "64 4" "512 1" "512 4" "2048 2"}; do
-  set -- $cfg
+  set -- ${cfg//_/ }
   for mode in ${MODES:-adaptive reservoir direct adaptive reservoir direct adaptive reservoir direct reference off}; do
     case $mode in
       adaptive)  H=device;        E="" ;;
