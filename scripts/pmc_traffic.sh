@@ -13,7 +13,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
     # WL = cfgN or cfgN-<ids mode> (bench.py --ids grouped|scattered)
     W=${WL%%-*}; IDS=range; [ "$W" != "$WL" ] && IDS=${WL#*-}
     timeout -k 10 240 rocprofv3 --pmc $C --output-format csv -d "$OUT/${WL}_$C" -o run -- \
-        python3 "$ROOT/bench.py" --workload "$W" --ids "$IDS" --steps 20 --warmup 2 --cpu-seconds 0 > "$OUT/${WL}_$C.log" 2>&1
+        python3 "$ROOT/bench.py" --workload "$W" --ids "$IDS" --steps 20 --warmup 2 --cpu-seconds 0 --companion-workload none > "$OUT/${WL}_$C.log" 2>&1
     rc=$?; echo "[$WL $C] rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
 done
