@@ -791,3 +791,47 @@ def test_window_tag_restart(built, torch_cuda):
             c.sync(s)
             bad = np.flatnonzero(pay.cpu().numpy() != want)
             assert bad.size == 0, (call, bad[:8], int(bad.size))
+
+
+def test_reservoir_failed_tail_loses_position_until_reseeded(built, monkeypatch):
+    """a reservoir tail crypt that fails must not let the slot go
+    on from an unknown keystream position.  With the test hook
+    ZRC4_KS_FAIL_TAIL_AFTER=2 the second tail crypt of the reservoir fails:
+    that call returns the error, every later call on the slot returns
+    ZRC4_ERR_STATE (-9) and touches nothing, another slot is unaffected, and
+    zrc4_ks_make_sbox reseeds it back to reference bytes."""
+    import ctypes as C
+    from zsummerx_amd import _capi
+    lib = _capi.load()
+    monkeypatch.setenv("ZRC4_KS_FAIL_TAIL_AFTER", "2")
+    ctx, ks = C.c_void_p(), C.c_void_p()
+    assert lib.zrc4_create(C.byref(ctx), 0, 256) == 0
+    try:
+        assert lib.zrc4_ks_create(ctx, 4096, C.byref(ks)) == 0
+        for slot, key in ((0, b"lost-slot"), (1, b"other-slot")):
+            assert lib.zrc4_ks_make_sbox(ks, slot, key, len(key)) == 0
+
+        def call(slot, n):
+            buf = (C.c_uint8 * n)()
+            ids = (C.c_uint32 * 1)(slot)
+            ptrs = (C.c_void_p * 1)(C.cast(buf, C.c_void_p))
+            lens = (C.c_uint32 * 1)(n)
+            return lib.zrc4_ks_crypt(ks, ids, ptrs, lens, 1), bytes(buf)
+
+        ref1 = pyoracle.Rc4(b"other-slot")
+        rc, out = call(1, 64)                          # tail 1: fine
+        assert rc == 0 and out == ref1.encryption(bytes(64))
+        rc, _ = call(0, 64)                            # tail 2: injected failure
+        assert rc != 0
+        for _ in range(3):
+            rc, out = call(0, 32)
+            assert rc == -9 and out == bytes(32)       # ZRC4_ERR_STATE, nothing crypted
+        assert lib.zrc4_ks_make_sbox(ks, 0, b"lost-slot", 9) == 0
+        rc, out = call(0, 100)                         # reseeded: reference bytes again
+        assert rc == 0 and out == pyoracle.Rc4(b"lost-slot").encryption(bytes(100))
+        rc, out = call(1, 50)
+        assert rc == 0 and out == ref1.encryption(bytes(50))
+    finally:
+        if ks:
+            lib.zrc4_ks_destroy(ks)
+        lib.zrc4_destroy(ctx)
