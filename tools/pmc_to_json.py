@@ -30,12 +30,14 @@ def per_dispatch(path, name_filter):
     return [(names[d], agg[d]) for d in sorted(agg)]
 
 
-def main(src="gpurun_out/traffic", tag="r02"):
+def main(src="gpurun_out/traffic", tag=None):
+    args = [a for a in sys.argv[1:] if not a.startswith("--round=")]
+    tag = tag or next((a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--round=")), "r03")
     src = ROOT / src
     calib = per_dispatch(src / "calib_FETCH_SIZE" / "run_counter_collection.csv", "calib_load_lane")
     calib_bytes = 1 << 30
     fetch_factor = statistics.median(v * 1024 / calib_bytes for _, v in calib)
-    for wl in sys.argv[1:] or ["cfg2", "cfg5"]:
+    for wl in args or ["cfg2", "cfg5"]:
         fr = per_dispatch(src / f"{wl}_FETCH_SIZE" / "run_counter_collection.csv", "zrc4::crypt_")[1:]
         wr = per_dispatch(src / f"{wl}_WRITE_SIZE" / "run_counter_collection.csv", "zrc4::crypt_")[1:]
         f, w = [v for _, v in fr], [v for _, v in wr]
