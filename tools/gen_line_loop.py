@@ -35,6 +35,7 @@ asserts that the result is the transpose.
 """
 from __future__ import annotations
 
+import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -223,7 +224,10 @@ def transpose_only(name: str, cur: int) -> str:
             f"#define ZRC4_LL_FINAL_{name} {fin}\n")
 
 
-def main():
+def main(ab_only: bool = False):
+    if ab_only:
+        write_ab()
+        return
     text = [
         "// GENERATED by tools/gen_line_loop.py -- do not edit by hand.\n",
         "// Throughput-regime message loop of crypt_kernel (zrc4_kernels.hpp,\n",
@@ -239,6 +243,11 @@ def main():
     ]
     OUT.write_text("".join(text))
     print("wrote", OUT)
+
+
+def write_ab():
+    """The timing-only variants are generated on demand (build_variant runs
+    this for ZRC4_LL_AB builds) and kept out of the tree."""
     ab = ["// GENERATED by tools/gen_line_loop.py -- do not edit by hand.\n",
           "// Timing-only A/B variants of zrc4_line_loop.inc (outputs are WRONG), selected by\n",
           "// ZRC4_LL_AB: 1 stores to the sink, 2 loads from the sink, 3 no transpose, 4 both sinks,\n",
@@ -246,9 +255,10 @@ def main():
           "#pragma once\n"]
     for v in (1, 2, 3, 4, 5, 6):
         ab += [f"#if ZRC4_LL_AB == {v}\n", half("P", P_BASE, v), half("Q", Q_BASE, v), "#endif\n"]
+    OUT_AB.parent.mkdir(exist_ok=True)
     OUT_AB.write_text("".join(ab))
     print("wrote", OUT_AB)
 
 
 if __name__ == "__main__":
-    main()
+    main(ab_only="--ab" in sys.argv[1:])

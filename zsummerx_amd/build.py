@@ -13,6 +13,7 @@ from __future__ import annotations
 import os
 import shutil
 import subprocess
+import sys
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -67,6 +68,10 @@ def build_variant(name: str, defines: dict, rev: str | None = None) -> Path:
     side in one process)."""
     out = PKG / f"libzrc4_{name}.so"
     srcs, inc, deps = HIP_SOURCES, ROOT / "include", HIP_DEPS
+    ab_inc = PKG / "csrc" / "ab" / "zrc4_line_loop_ab.inc"
+    if defines.get("ZRC4_LL_AB") and not rev and not ab_inc.exists():
+        # timing-only variants, generated on demand (tools/gen_line_loop.py --ab)
+        subprocess.run([sys.executable, str(ROOT / "tools" / "gen_line_loop.py"), "--ab"], check=True)
     if rev and not (ROOT / ".git").exists():      # the GPU box: no history, use the prebuilt library
         if not out.exists():
             raise FileNotFoundError(f"{out} (revision {rev}) must be built before the GPU run")
