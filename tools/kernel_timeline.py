@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Where a crypt_kernel launch spends its time, per wave (diagnostic build).
+"""Where a crypt_kernel / crypt_win_kernel launch spends its time, per wave
+(diagnostic build).
 
 Builds libzrc4 with ZRC4_TIMING=1 (zrc4_kernels.hpp, Stamps): lane 0 of every
 wave stamps s_memrealtime (100 MHz) and s_memtime (shader clock) at kernel
@@ -165,8 +166,12 @@ def main():
         rc = hip.hipMemcpy(C.c_void_p(hwid.ctypes.data), C.c_void_p(sink.value + 65536), C.c_size_t(hwid.nbytes), 2)
         if rc:
             raise SystemExit(f"hipMemcpy failed {rc}")
-        waves = (S + 63) // 64
-        act = np.array([(w % 4) < args.active_waves for w in range(waves)])
+        if S <= 32 * 256:        # crypt_win_kernel (<= 32 groups): one record per 4-stream workgroup
+            waves = S // 4
+            act = np.ones(waves, dtype=bool)
+        else:
+            waves = (S + 63) // 64
+            act = np.array([(w % 4) < args.active_waves for w in range(waves)])
         out[wl] = summarise(rec[:waves][act], int(act.sum()), L)
         out[wl]["active_waves_per_group"] = args.active_waves
         out[wl]["ids"] = args.ids

@@ -116,16 +116,16 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
         const zrc4::FrameArgs fa = fr ? *fr : zrc4::FrameArgs{};
         if (mode == zrc4::kRange && fr)
             hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kRange, true>), wgrid, wblk, 0, s, c->arena, c->xy, ids,
-                               first_slot, payload, off, len, n, c->capacity, c->err, fa, cl);
+                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl);
         else if (mode == zrc4::kRange)
             hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kRange, false>), wgrid, wblk, 0, s, c->arena, c->xy, ids,
-                               first_slot, payload, off, len, n, c->capacity, c->err, fa, cl);
+                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl);
         else if (fr)
             hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kGrouped, true>), wgrid, wblk, 0, s, c->arena, c->xy,
-                               ids, first_slot, payload, off, len, n, c->capacity, c->err, fa, cl);
+                               ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl);
         else
             hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kGrouped, false>), wgrid, wblk, 0, s, c->arena, c->xy,
-                               ids, first_slot, payload, off, len, n, c->capacity, c->err, fa, cl);
+                               ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl);
         return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
     }
     // Few whole groups: half-group workgroups, one per CU (2 waves per CU).

@@ -220,8 +220,10 @@ __global__ void __launch_bounds__(64)
 crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const uint32_t *__restrict__ ids,
                  uint32_t first_slot, uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
                  const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity, uint32_t *__restrict__ err,
-                 FrameArgs fr, Claim cl)
+                 uint8_t *__restrict__ sink, FrameArgs fr, Claim cl)
 {
+    Stamps ts;                                   // ZRC4_TIMING builds only (zrc4_kernels.hpp)
+    stamp(ts, 0);
     __shared__ __attribute__((aligned(1024))) uint32_t Mk[kWinStreams * 256];
     __shared__ __attribute__((aligned(kWinRing))) uint8_t Ring[kWinStreams * kWinRing];
     __shared__ __attribute__((aligned(256))) uint8_t Sb[kWinStreams * 256];
@@ -356,6 +358,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
 #pragma unroll
     for (int i = 0; i < 4; ++i) reinterpret_cast<uint4 *>(Mk)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
+    stamp(ts, 1);
 
     const uint32_t sb = (uint32_t)(uintptr_t)S, mb = (uint32_t)(uintptr_t)M, rb = (uint32_t)(uintptr_t)R;
     WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
@@ -399,6 +402,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
         }
     }
 
+    stamp(ts, 2);
     if (valid && l == 0) xy[slot] = (uint16_t)(((w.xa - 1u) & 0xFFu) | ((w.y & 0xFFu) << 8));
     if constexpr (FRAME) {
         // the stream's 16 lanes stored its bytes: they must have landed
@@ -416,6 +420,13 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
                            ((uint32_t)Sb[768u + kk] << 24);
         *reinterpret_cast<uint32_t *>(img + (size_t)kk * 256u) = v;
     }
+#if ZRC4_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    stamp(ts, 3);
+    stamps_out(ts, sink, wg * 64u + q);          // record of the workgroup's column
+#else
+    (void)sink;
+#endif
 }
 
 }  // namespace zrc4
