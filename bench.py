@@ -348,6 +348,11 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
                      "algorithmic_bytes_per_launch": B,
                      "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                      "kernel_min_segment_us": round(min(kern_ms) * 1e3, 3),
+                     # the first event to the last over the whole timed region, per step:
+                     # every launch and inter-launch gap, not the host's first-launch
+                     # latency or its wake-up after the last kernel (ms_per_step has both)
+                     "device_us_per_step": round(sum(k * min(args.event_every, args.steps - i * args.event_every)
+                                                     for i, k in enumerate(kern_ms)) / args.steps * 1e3, 3),
                      "kernel_timing": f"HIP events bracketing {len(kern_ms)} segments of "
                                       f"{args.event_every} back-to-back timed launches (per-launch average)"},
         "latency_ceiling_gibs": {"note": "chain-bound payload rate min(S,131072 resident)*2.4GHz/L_cyc per "

@@ -135,6 +135,8 @@ def test_self_launch_two_ranks(capsys):
     assert res["config"]["world_size_seen"] == 2 and res["config"]["dist_backend"] == "gloo"
     assert res["config"]["curve"].startswith("weak")
     assert [g["rank"] for g in res["per_gpu"]] == [0, 1]
+    rf = res["roofline"]              # the device span per step: launches and gaps, no host wake-up
+    assert 0 < rf["device_us_per_step"] <= res["ms_per_step"] * 1e3 * 1.05
     comp = res["configs4_strong"]
     assert comp["n_gpus"] == 2 and comp["scaling"] == "strong"
     assert comp["config"]["sessions_per_gpu"] == 256 and comp["config"]["global_sessions_per_step"] == 512
