@@ -446,6 +446,49 @@ def test_window_path_ragged(built, torch_cuda, first_slot, n):
         assert c.get_state(nslot) == neighbour
 
 
+# ----------------------------------- every kernel-choice boundary of launch_crypt
+@pytest.mark.parametrize("first_slot,n", [
+    (0, 32 * 256), (0, 32 * 256 + 1),          # last window batch / first half-group batch
+    (0, 128 * 256), (0, 128 * 256 + 1),        # last half-group batch (2G <= 256 CUs) / first whole-group
+    (0, 256 * 256), (0, 256 * 256 + 1),        # last one-group-per-CU batch / first throughput batch
+    (100, 20 * 256),                           # few groups but unaligned: no window kernel
+])
+def test_dispatch_boundaries_bit_exact(built, torch_cuda, first_slot, n):
+    """zrc4.hip launch_crypt picks the kernel from the batch's group count
+    and alignment (window <= 32 aligned groups, half-group while 2G <= CUs,
+    whole-group while G <= CUs, the persistent throughput kernel above).
+    Each side of every boundary, with ragged lengths (0..1 500, unaligned
+    starts, untouched gaps), two calls in a row and states checked after."""
+    torch = torch_cuda
+    rng = np.random.default_rng(41 + n + first_slot)
+    keys = rng.integers(0, 256, 16 * n, dtype=np.uint8)
+    koff = np.arange(n, dtype=np.uint64) * 16
+    klen = np.full(n, 16, dtype=np.uint32)
+    ob = pyoracle.Batch(n)
+    ob.make_sbox(keys, koff, klen)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    s = torch.cuda.current_stream()
+    with Context(0, first_slot + n + 256) as c:
+        c.ksa_range(first_slot, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
+        for call in range(2):
+            L = rng.integers(0, 1500, n).astype(np.uint32)
+            L[rng.random(n) < 0.05] = 0
+            gaps = rng.integers(0, 24, n)
+            off = np.cumsum(np.concatenate([[gaps[0]], L[:-1] + gaps[1:]])).astype(np.uint64)
+            data = rng.integers(0, 256, int(off[-1] + L[-1]) + 64, dtype=np.uint8)
+            want = data.copy()
+            ob.crypt(want, off, L, threads=8)
+            pay = T(data)
+            c.crypt_range(first_slot, pay, T(off.view(np.int64)), T(L.view(np.int32)), stream=s)
+            c.sync(s)
+            bad = np.flatnonzero(pay.cpu().numpy() != want)
+            assert bad.size == 0, (call, bad[:8], int(bad.size))
+        for i in sorted({0, 255, n // 2, n - 2, n - 1}):
+            sb, x, y = c.get_state(first_slot + i)
+            want_sb, wx, wy = ob.state(i)
+            assert (sb, x, y) == (bytes(want_sb), wx, wy), i
+
+
 # ------------------------------------------ grouped ids (zrc4_crypt_grouped)
 def grouped_batch(rng, n_groups, groups_total, fill=(1, 256)):
     """Buckets of 256 entries: bucket b takes a random subset (random order)
