@@ -81,9 +81,14 @@ def by_place(rt: np.ndarray, hwid: np.ndarray, wgs: int, K: int) -> dict:
             uneq.append((abs(chain[a] - chain[b]), int(simd[a]), int(simd[b]), round(float(chain[a]), 1),
                          round(float(chain[b]), 1)))
     if means:
+        two = [ix for ix in pairs.values() if len(ix) == 2]
         out["cu_pairs"] = {"std_of_cu_means": round(float(np.std(means)), 2),
                            "mean_abs_diff_in_pair": round(float(np.mean(diffs)), 2),
-                           "most_unequal": [list(u[1:]) for u in sorted(uneq)[-8:]]}
+                           "most_unequal": [list(u[1:]) for u in sorted(uneq)[-8:]],
+                           # which workgroup ids share a CU (for grid-half / parity staggers)
+                           "split_by_half": round(sum((a < wgs // 2) != (b < wgs // 2) for a, b in two) / len(two), 3),
+                           "split_by_parity": round(sum((a & 1) != (b & 1) for a, b in two) / len(two), 3),
+                           "sample": [sorted(ix) for ix in two[:8]]}
     order = np.argsort(chain)
     out["fastest"] = [[int(xcc[i]), int(se[i]), int(cu[i]), round(float(chain[i]), 2)] for i in order[:6]]
     out["slowest"] = [[int(xcc[i]), int(se[i]), int(cu[i]), round(float(chain[i]), 2)] for i in order[-6:]]
