@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--footprint-mib", type=int, default=1200)
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--define", action="append", default=[], help="extra -D for the timing build (NAME=V)")
+    ap.add_argument("--dump", default="", help="save the raw per-workgroup stamps (npz) under this prefix")
     args = ap.parse_args()
     from zsummerx_amd import build
     defs = {"ZRC4_TIMING": "1"}
@@ -163,6 +164,8 @@ def main():
         out[wl]["last_launch_event_us"] = round(last_event_us, 2)
         out[wl]["by_place"] = by_place(rt, hwid, wgs, min(7, groups // wgs))
         print(wl, json.dumps(out[wl]), flush=True)
+        if args.dump:
+            np.savez(f"{args.dump}_{wl}.npz", rt=rt[:wgs], clk=clk[:wgs], hwid=hwid[:wgs])
         lib.zrc4_destroy(h)
         del keys, pay, off, ln, klen, koff
         torch.cuda.empty_cache()
