@@ -467,6 +467,18 @@ def cpu_baseline(args, S, L):
 
 
 # ------------------------------------------------------- host-inclusive rate
+def host_chunks(nbytes: int) -> int:
+    """Default pipelining depth of the copy path (r03, tools/hostinc_sweep.py,
+    profiles/r03/hostinc_sweep.log and hostinc/): the box's pinned copies run
+    at ~57 GB/s whether one direction or both are busy, so chunking only hides
+    the kernel (25 us to 0.3 ms against 0.15-19 ms of copies) and costs a
+    per-copy latency: whole batches up to 32 MiB (cfg2 18.4 GiB/s whole vs
+    11.1 in 8 chunks), one chunk per 32 MiB above, at most 16 (cfg5 29.9 in
+    16 chunks on 4 streams vs 26.2 whole)."""
+    mib = nbytes >> 20
+    return 1 if mib <= 32 else max(1, min(16, mib // 32))
+
+
 def host_inclusive(args):
     """The path starts in a socket recv buffer and ends in a send buffer, so
     the rate including PCIe is measured too (reported in DESIGN.md, never as
@@ -488,7 +500,8 @@ def host_inclusive(args):
     devbuf = torch.empty(S * L, dtype=torch.uint8, device=dev)
     off = T(w.off.view(np.int64))
     ln = T(w.length.view(np.int32))
-    nchunk = max(1, min(args.chunks, S // 256))
+    chunks = args.chunks or host_chunks(S * L)
+    nchunk = max(1, min(chunks, S // 256))
     per = -(-S // nchunk)
     per = -(-per // 256) * 256                      # whole 256-slot groups per chunk
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
@@ -746,8 +759,10 @@ def parse(argv=None):
                         "(strong scaling, BASELINE configs[4]) as 'configs4_strong'; none disables")
     p.add_argument("--companion-steps", type=int, default=100)
     p.add_argument("--companion-warmup", type=int, default=120)
-    p.add_argument("--chunks", type=int, default=8)
-    p.add_argument("--streams", type=int, default=3)
+    p.add_argument("--chunks", type=int, default=0,
+                   help="with --host-inclusive: chunks of the batch (0 = by size: one up to 8 MiB, else one per "
+                        "2 MiB up to 16; tools/hostinc_sweep.py)")
+    p.add_argument("--streams", type=int, default=4)
     return p.parse_args(argv)
 
 
