@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$PWD
-OUT=gpurun_out/r03/final
+OUT=${VAL_OUT:-gpurun_out/r03/final}
 mkdir -p $OUT
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {  # name, seconds, command...
