@@ -432,13 +432,16 @@ def usable_cpus():
 
 
 def cpu_baseline(args, S, L):
-    """The oracle restatement (a -O3 C port of rc4_encryption.h:74-93) timed on
-    this host on a bounded sample of the same workload (same keys, payload and
+    """The reference's own RC4 (RC4Encryption from depends/rc4/rc4_encryption.h,
+    compiled -O3 from where it lies into oracle/_ref/libzrc4_ref.so; kind
+    "reference") -- or, where that build is absent, the oracle restatement (a
+    -O3 C port of rc4_encryption.h:74-93; kind "port") -- timed on this host
+    on a bounded sample of the same workload (same keys, payload and
     pre-advance as rank 0's first batch): 1 thread (the reference's single
     event-loop thread), then one worker per CPU the process can use at once
     (usable_cpus: affinity mask capped by the cgroup quota), each re-crypting
-    its round-robin share for the whole window (one thread start per worker).
-    Reported, not optimised against."""
+    its contiguous share for the whole window.  Reported, not optimised
+    against."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle  # cpu_baseline leg only
     from zsummerx_amd import synth
@@ -447,9 +450,16 @@ def cpu_baseline(args, S, L):
     if args.cpu_threads > 0:
         cores = min(cores, args.cpu_threads)
     w = synth.make(0, S, L, threads=8)
-    ob = pyoracle.Batch(S)
-    ob.make_sbox(w.keys, w.key_off, w.key_len)
-    ob.crypt(np.zeros(1000, dtype=np.uint8), np.zeros(S, dtype=np.uint64), w.adv)
+    if pyoracle.ref_lib() is not None:
+        kind, ob = "reference", pyoracle.RefBatch(S)
+        ob.make_sbox(w.keys, w.key_off, w.key_len)
+        ob.advance(w.adv)
+        what = "RC4Encryption::encryption, the reference header compiled -O3 (oracle/_ref)"
+    else:
+        kind, ob = "port", pyoracle.Batch(S)
+        ob.make_sbox(w.keys, w.key_off, w.key_len)
+        ob.crypt(np.zeros(1000, dtype=np.uint8), np.zeros(S, dtype=np.uint64), w.adv)
+        what = "the oracle restatement of rc4_encryption.h:74-93 (-O3); oracle/_ref absent"
     pay = w.payload.copy()
     reps = 5
     win = args.cpu_seconds / 2 / reps
@@ -459,11 +469,11 @@ def cpu_baseline(args, S, L):
 
     one = rate(1)
     many = rate(cores) if cores > 1 else one
-    return {"value": round(many, 4), "unit": "GiB/s", "cores": cores, "threads": cores, "kind": "port",
+    return {"value": round(many, 4), "unit": "GiB/s", "cores": cores, "threads": cores, "kind": kind,
             "value_1thread": round(one, 4), "hardware_concurrency": os.cpu_count(),
             "affinity_cores": aff, "cgroup_cpu_quota": quota,
-            "sample": f"{args.workload} batch ({S} x {L} B) re-crypted for {win:.1f} s windows, median of {reps}: "
-                      f"1 thread, then {cores} threads (min(affinity {aff}, ceil(cgroup quota {quota})))"}
+            "sample": f"{what}: {args.workload} batch ({S} x {L} B) re-crypted for {win:.1f} s windows, median of "
+                      f"{reps}: 1 thread, then {cores} threads (min(affinity {aff}, ceil(cgroup quota {quota})))"}
 
 
 # ------------------------------------------------------- host-inclusive rate

@@ -70,6 +70,8 @@ def ref_lib():
         R.zrc4_ref_get_state.argtypes = [_P, _P, _P, _P]
         R.zrc4_ref_crypt_batch.argtypes = [_P, _P, _P, _P, C.c_uint32]
         R.zrc4_ref_crypt_batch.restype = C.c_double
+        R.zrc4_ref_crypt_rate.argtypes = [_P, _P, _P, _P, C.c_uint32, C.c_int, C.c_double]
+        R.zrc4_ref_crypt_rate.restype = C.c_double
         R.zrc4_ref_has_raw_packet.argtypes = [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
         _ref = R
     return _ref
@@ -141,6 +143,45 @@ class RefRc4:
         x, y = C.c_uint8(), C.c_uint8()
         self.R.zrc4_ref_get_state(self.mem, sb, C.byref(x), C.byref(y))
         return bytes(sb), x.value, y.value
+
+
+class RefBatch:
+    """n streams of the REAL reference class in one array (oracle/_ref), for
+    the CPU baseline (bench.py cpu_baseline, kind "reference")."""
+
+    def __init__(self, n: int):
+        R = ref_lib()
+        if R is None:
+            raise FileNotFoundError(f"{REF_LIB} not built (needs /root/reference)")
+        self.R, self.n, self.sz = R, n, R.zrc4_ref_state_size()
+        self.mem = (C.c_uint8 * (self.sz * n))()
+        self.base = C.addressof(self.mem)
+
+    def make_sbox(self, keys: np.ndarray, key_off: np.ndarray, key_len: np.ndarray) -> None:
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        for i in range(self.n):
+            o = int(key_off[i])
+            self.R.zrc4_ref_make_sbox(C.c_void_p(self.base + i * self.sz), C.c_void_p(keys.ctypes.data + o),
+                                      int(key_len[i]))
+
+    def advance(self, adv: np.ndarray) -> None:
+        """Pre-advance stream i by adv[i] keystream bytes (encryption over zeros)."""
+        scratch = np.zeros(int(np.max(adv)) if len(adv) else 1, dtype=np.uint8)
+        for i in range(self.n):
+            if adv[i]:
+                self.R.zrc4_ref_encryption(C.c_void_p(self.base + i * self.sz), C.c_void_p(scratch.ctypes.data),
+                                           int(adv[i]))
+
+    def crypt_rate(self, payload: np.ndarray, off: np.ndarray, length: np.ndarray, threads: int,
+                   seconds: float) -> float:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        r = self.R.zrc4_ref_crypt_rate(C.c_void_p(self.base), C.c_void_p(payload.ctypes.data),
+                                       C.c_void_p(off.ctypes.data), C.c_void_p(length.ctypes.data), self.n,
+                                       int(threads), float(seconds))
+        if r <= 0:
+            raise RuntimeError("zrc4_ref_crypt_rate failed")
+        return r
 
 
 def py_rc4(key: bytes, data: bytes, skip: int = 0) -> bytes:

@@ -3,7 +3,8 @@
 // Compiles the REAL reference RC4 (/root/reference/depends/rc4/rc4_encryption.h,
 // included where it lies, never copied) behind a tiny extern "C" surface so the
 // golden-fixture generator (tests/golden/make_golden.py) and the CPU-only tests
-// can run the reference itself.  Built by oracle/Makefile into
+// can run the reference itself, and so that bench.py's cpu_baseline leg can
+// time it (zrc4_ref_crypt_rate).  Built by oracle/Makefile into
 // oracle/_ref/libzrc4_ref.so, only when /root/reference is present.
 //
 // The reference header includes nothing itself; its includers provide <string>
@@ -12,6 +13,9 @@
 #include <cstring>
 #include <cstdint>
 #include <chrono>
+#include <atomic>
+#include <thread>
+#include <vector>
 #include <rc4/rc4_encryption.h>
 #include <proto4z/proto4z.h>   // HasRawPacket (depends/proto4z/proto4z.h:704-748), header-only
 
@@ -57,6 +61,48 @@ double zrc4_ref_crypt_batch(void *states, uint8_t *payload, const uint64_t *off,
     for (uint32_t i = 0; i < n; ++i) s[i].encryption(payload + off[i], (int)len[i]);
     auto t1 = std::chrono::steady_clock::now();
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// CPU baseline (bench.py cpu_baseline, kind "reference"): `threads` workers,
+// worker t re-crypting its contiguous share of the n sessions through the
+// reference's encryption() until `seconds` have passed, all released at once;
+// returns payload bytes per second over the common window.
+double zrc4_ref_crypt_rate(void *states, uint8_t *payload, const uint64_t *off, const uint32_t *len,
+                           uint32_t n, int threads, double seconds)
+{
+    if (threads < 1) threads = 1;
+    if ((uint32_t)threads > n) threads = (int)n;
+    RC4Encryption *s = static_cast<RC4Encryption *>(states);
+    std::atomic<int> ready(0);
+    std::atomic<bool> go(false);
+    std::vector<unsigned long long> bytes((size_t)threads, 0ull);
+    std::vector<std::thread> pool;
+    typedef std::chrono::steady_clock clk;
+    clk::time_point deadline;
+    for (int t = 0; t < threads; ++t) {
+        pool.emplace_back([&, t]() {
+            const uint32_t b = (uint32_t)((uint64_t)n * t / threads), e = (uint32_t)((uint64_t)n * (t + 1) / threads);
+            unsigned long long done = 0;
+            ready.fetch_add(1);
+            while (!go.load(std::memory_order_acquire)) {}
+            while (clk::now() < deadline) {
+                for (uint32_t i = b; i < e; ++i) {
+                    s[i].encryption(payload + off[i], (int)len[i]);
+                    done += len[i];
+                }
+            }
+            bytes[(size_t)t] = done;
+        });
+    }
+    while (ready.load() != threads) {}
+    const clk::time_point t0 = clk::now();
+    deadline = t0 + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double>(seconds));
+    go.store(true, std::memory_order_release);
+    for (auto &th : pool) th.join();
+    const double dt = std::chrono::duration<double>(clk::now() - t0).count();
+    unsigned long long total = 0;
+    for (unsigned long long v : bytes) total += v;
+    return (double)total / dt;
 }
 
 // zsummer::proto4z::HasRawPacket -- the reference's framing check, as

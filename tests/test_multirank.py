@@ -165,3 +165,43 @@ def test_usable_cpus_caps_affinity_by_quota(monkeypatch):
     assert bench.usable_cpus()[0] == 3
     monkeypatch.setattr(bench, "cgroup_cpu_quota", lambda: None)
     assert bench.usable_cpus()[0] == 256
+
+
+def test_cpu_baseline_times_the_reference(monkeypatch):
+    """bench.py's cpu_baseline leg times the reference's own RC4Encryption
+    (oracle/_ref, kind "reference") when that build is present, else the
+    restatement (kind "port"); the reported threads are the usable CPUs."""
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import bench
+    import pyoracle
+    monkeypatch.setattr(bench, "usable_cpus", lambda: (2, 8, 2.0))
+    args = bench.parse(["--cpu-seconds", "0.2", "--workload", "cfg2"])
+    r = bench.cpu_baseline(args, 512, 1024)
+    assert r["kind"] == ("reference" if pyoracle.ref_lib() is not None else "port")
+    assert r["cores"] == r["threads"] == 2 and r["value"] > 0 and r["value_1thread"] > 0
+    assert r["sample"].startswith("RC4Encryption" if r["kind"] == "reference" else "the oracle")
+
+
+def test_reference_batch_matches_the_restatement():
+    """The reference-timed baseline crypts the same bytes as the restatement."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import ctypes as C
+    import pyoracle
+    if pyoracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built")
+    from zsummerx_amd import synth
+    S, L = 64, 300
+    w = synth.make(0, S, L, threads=1)
+    rb = pyoracle.RefBatch(S)
+    rb.make_sbox(w.keys, w.key_off, w.key_len)
+    rb.advance(w.adv)
+    ob = pyoracle.Batch(S)
+    ob.make_sbox(w.keys, w.key_off, w.key_len)
+    ob.crypt(np.zeros(1000, dtype=np.uint8), np.zeros(S, dtype=np.uint64), w.adv)
+    p1, p2 = w.payload.copy(), w.payload.copy()
+    for i in range(S):
+        rb.R.zrc4_ref_encryption(C.c_void_p(rb.base + i * rb.sz), C.c_void_p(p1.ctypes.data + int(w.off[i])),
+                                 int(w.length[i]))
+    ob.crypt(p2, w.off, w.length)
+    assert np.array_equal(p1, p2)
