@@ -955,10 +955,21 @@ __device__ __forceinline__ void frame_walk(const uint8_t *b, uint32_t L, uint32_
 #ifndef ZRC4_WPERM
 #define ZRC4_WPERM 97
 #endif
+#ifndef ZRC4_WMAP
+#define ZRC4_WMAP 1
+#endif
 constexpr uint32_t kTabOff = kGroupBytes + 16;
 constexpr uint32_t kSidOff = kTabOff + 256 * 16;              // 16 B: the half-group workgroup's SIMD ids
 constexpr uint32_t kSmemDirect = kSidOff + 16;                // 69 664 B: two workgroups per CU
 constexpr uint32_t kSmemHalf = 96 * 1024;                     // one workgroup per CU
+
+// Workgroup k runs on XCD k mod 8.  xcd_run_map deals the groups so that
+// each XCD takes runs of 8 consecutive groups per 64: k = 64s + 8r + x ->
+// 64s + 8x + r (bijective; a tail of grid mod 64 groups keeps its order).
+__device__ __forceinline__ uint32_t xcd_run_map(uint32_t k, uint32_t grid)
+{
+    return k >= (grid & ~63u) ? k : (k & ~63u) | ((k & 7u) << 3) | ((k >> 3) & 7u);
+}
 
 template <int MODE, bool FRAME, bool HALF>
 __device__ __forceinline__ void
@@ -1005,18 +1016,25 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         if (w != a && w != b) return;                    // uniform (SGPR) branch: the wave ends
         tid = (w == a ? 0u : 64u) + (threadIdx.x & 63u);
     }
-    // Which group (bucket) this workgroup runs: blockIdx.x, or (ZRC4_WPERM,
-    // whole groups) blockIdx.x * ZRC4_WPERM mod grid -- a bijection when the
-    // prime ZRC4_WPERM does not divide the grid -- so that the XCD a
-    // workgroup lands on (blockIdx.x mod 8) no longer follows the group
-    // order: cfg3 23.29 -> 22.72 us (profiles/r02/ab_wperm.log; a grouped
-    // batch, whose buckets come in random group order, moved 1.01x its
-    // algorithmic bytes against 1.10x for the same range batch).
+    // Which group (bucket) this workgroup runs.  Whole-group launches deal
+    // the groups to the XCDs in runs of 8 consecutive groups (xcd_run_map,
+    // ZRC4_WMAP, r03): with workgroup k -> group k (or r02's 97k mod grid,
+    // ZRC4_WMAP=0) XCD x ran only the groups = x mod 8, whose payload and
+    // images sit at one offset modulo 8 groups, and the XCD's L2 evicted the
+    // lanes' partly written 128-byte lines early: 1.25x the algorithmic write
+    // bytes at 256-byte messages, 1.00x with the runs; 65 536 x 1 KiB 60.5 ->
+    // 57.2 us, x 2 KiB 110.7 -> 100.3; cfg3 22.9 -> 23.5 (same-process
+    // medians, profiles/r03/wmap/).  Half-group launches keep k -> (k/2, k%2)
+    // (their A/B was neutral to +2.5 %).
     uint32_t wg = blockIdx.x;
+#if ZRC4_WMAP
+    if constexpr (!HALF) wg = xcd_run_map(blockIdx.x, gridDim.x);
+#else
     if constexpr (!HALF && ZRC4_WPERM != 0) {
         constexpr uint32_t kMul = ZRC4_WPERM + 0u;
         if (gridDim.x % kMul != 0u) wg = (blockIdx.x * kMul) % gridDim.x;
     }
+#endif
 #if defined(ZRC4_STAGGER) && ZRC4_STAGGER
     // A/B diagnostic (cfg3 write traffic): workgroup start spread over
     // 0..7 x ZRC4_STAGGER x 64 cycles, as a grouped launch's longer prologue spreads it
@@ -1025,7 +1043,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #endif
     const uint32_t e = wg * kLanes + tid;                // batch entry of this thread
     const bool valid = e < n;
-    const uint32_t h = HALF ? (blockIdx.x & 1u) : 0u;    // half of the group (HALF)
+    const uint32_t h = HALF ? (wg & 1u) : 0u;            // half of the group (HALF)
     const uint32_t j = h * 128u + tid;                   // group lane
     const uint32_t vo0 = image_lane_offset(tid, HALF, h);
     const uint32_t col = col_of(j);
@@ -1041,7 +1059,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         // Issued from asm, first: hipcc otherwise sinks these loads below its
         // wait for len/off.  Group (first_slot >> 8) + w lies inside the arena
         // even when first_slot is unaligned and the image goes unused.
-        g = (first_slot >> 8) + (HALF ? blockIdx.x >> 1 : wg);
+        g = (first_slot >> 8) + (HALF ? wg >> 1 : wg);
         issue_image_asm(ilo, ihi, arena + (size_t)g * kGroupBytes, vo0);
         whole = (first_slot & 255u) == 0u;
         ent = e;
@@ -1056,7 +1074,7 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         //    across waves by one atomic min/max per wave) and the slot ->
         //    entry table; 3. lane j takes the entry of slot g*256 + j.
         constexpr uint32_t kPer = kGroup / kLanes;
-        const uint32_t w = HALF ? blockIdx.x >> 1 : wg;
+        const uint32_t w = HALF ? wg >> 1 : wg;
         uint32_t *te = reinterpret_cast<uint32_t *>(smem + kTabOff);          // entry index
         uint32_t *tl = te + 256;                                              // length
         uint64_t *to = reinterpret_cast<uint64_t *>(smem + kTabOff + 2048);   // offset
