@@ -78,8 +78,10 @@ double zrc4_ref_crypt_rate(void *states, uint8_t *payload, const uint64_t *off, 
     std::vector<unsigned long long> bytes((size_t)threads, 0ull);
     std::vector<std::thread> pool;
     typedef std::chrono::steady_clock clk;
-    clk::time_point deadline;
-    for (int t = 0; t < threads; ++t) {
+    clk::time_point deadline = clk::now();   // workers read it only after `go`
+    bool failed = false;
+    for (int t = 0; t < threads && !failed; ++t) {
+        try {
         pool.emplace_back([&, t]() {
             const uint32_t b = (uint32_t)((uint64_t)n * t / threads), e = (uint32_t)((uint64_t)n * (t + 1) / threads);
             unsigned long long done = 0;
@@ -93,6 +95,14 @@ double zrc4_ref_crypt_rate(void *states, uint8_t *payload, const uint64_t *off, 
             }
             bytes[(size_t)t] = done;
         });
+        } catch (...) {          // no thread: release the started ones at once and report failure
+            failed = true;
+        }
+    }
+    if (failed) {
+        go.store(true, std::memory_order_release);
+        for (auto &th : pool) th.join();
+        return -1.0;
     }
     while (ready.load() != threads) {}
     const clk::time_point t0 = clk::now();
