@@ -127,9 +127,12 @@ def zl_block(base: int) -> str:
 def half(name: str, cur: int, ab: int = 0) -> str:
     """ab (timing-only A/B builds, zrc4_line_loop_ab.inc; outputs are wrong):
     1 stores to the lane's sink slot (one 64 KiB sink for the whole chip:
-    contended), 2 loads from it, 3 no transpose, 4 both sinks, 5 no stores (a
-    sink load in place of each, so the vmcnt counts hold), 6 = 5 + loads from
-    the sink."""
+    contended), 2 loads from it, 3 no transpose, 4 both sinks.  (r02's 5 / 6,
+    a sink load in place of each store, were removed in r03: those loads
+    landed in the store-address temporaries v144-v151 asynchronously, and
+    crypt_last_half_next_asm ends on vmcnt(8), so they could still be in
+    flight when the compiler reused those registers -- a cfg5 A/B run with
+    them faulted the GPU.)"""
     start = {c: cur + 4 * c for c in range(8)}
     tl, final, ops, _ = transpose_plan(start, [X_BASE + 4 * t for t in range(4)])
     simulate(ops, start, final)
@@ -180,10 +183,7 @@ def half(name: str, cur: int, ab: int = 0) -> str:
         w(q(f"v_cndmask_b32_e64 v{sa + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
         if ab in (1, 4):
             sa = SINK
-        if ab in (5, 6):     # no store: a sink load keeps the vmcnt counts
-            w(f'"global_load_dword v{sa}, v[{SINK}:{SINK + 1}], off\\n\\t"')
-        else:
-            w(f'"global_store_dwordx4 v[{sa}:{sa + 1}], v[{final[qq]}:{final[qq] + 3}], off nt\\n\\t"')
+        w(f'"global_store_dwordx4 v[{sa}:{sa + 1}], v[{final[qq]}:{final[qq] + 3}], off nt\\n\\t"')
     for qq in range(8):
         a = ADDR_BASE + 2 * qq
         w(q(f"v_lshl_add_u64 v[{a}:{a + 1}], 8, 4, v[{a}:{a + 1}]"))     # += 8 << 4 (shift must be 0..4)
@@ -195,8 +195,8 @@ def half(name: str, cur: int, ab: int = 0) -> str:
     w(q("v_cmp_lt_u32_e64 %[msk], %[s1], %[nblk]"))
     w(q(f"v_cndmask_b32_e64 v{LA}, v{SINK}, %[palo], %[msk]"))
     w(q(f"v_cndmask_b32_e64 v{LA + 1}, v{SINK + 1}, %[pahi], %[msk]"))
-    la = SINK if ab in (2, 4, 6) else LA
-    lb = SINK if ab in (2, 4, 6) else LB
+    la = SINK if ab in (2, 4) else LA
+    lb = SINK if ab in (2, 4) else LB
     for d in range(4):
         w(f'"global_load_dwordx4 v[{cur + 4 * d}:{cur + 4 * d + 3}], v[{la}:{la + 1}], off offset:{16 * d}\\n\\t"')
     w(q("s_add_u32 %[s1], %[sb], 5"))
@@ -250,10 +250,9 @@ def write_ab():
     this for ZRC4_LL_AB builds) and kept out of the tree."""
     ab = ["// GENERATED by tools/gen_line_loop.py -- do not edit by hand.\n",
           "// Timing-only A/B variants of zrc4_line_loop.inc (outputs are WRONG), selected by\n",
-          "// ZRC4_LL_AB: 1 stores to the sink, 2 loads from the sink, 3 no transpose, 4 both sinks,\n",
-          "// 5 no stores, 6 no stores + loads from the sink.\n",
+          "// ZRC4_LL_AB: 1 stores to the sink, 2 loads from the sink, 3 no transpose, 4 both sinks.\n",
           "#pragma once\n"]
-    for v in (1, 2, 3, 4, 5, 6):
+    for v in (1, 2, 3, 4):
         ab += [f"#if ZRC4_LL_AB == {v}\n", half("P", P_BASE, v), half("Q", Q_BASE, v), "#endif\n"]
     OUT_AB.parent.mkdir(exist_ok=True)
     OUT_AB.write_text("".join(ab))
