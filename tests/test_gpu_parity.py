@@ -452,6 +452,8 @@ def test_window_path_ragged(built, torch_cuda, first_slot, n):
     (0, 128 * 256), (0, 128 * 256 + 1),        # last half-group batch (2G <= 256 CUs) / first whole-group
     (0, 256 * 256), (0, 256 * 256 + 1),        # last one-group-per-CU batch / first throughput batch
     (100, 20 * 256),                           # few groups but unaligned: no window kernel
+    (0, 200 * 256 - 7),                        # whole-group kernel: 3 XCD-run blocks of 64 + a tail of 8
+    (37, 150 * 256),                           # unaligned range over 151 groups (gathered columns, runs + tail)
 ])
 def test_dispatch_boundaries_bit_exact(built, torch_cuda, first_slot, n):
     """zrc4.hip launch_crypt picks the kernel from the batch's group count
