@@ -369,25 +369,28 @@ WIN_MAX_GROUPS = 32   # zrc4.hip ZRC4_WIN_MAX_GROUPS
 
 def kernel_name(S: int, ids: str = "range") -> str:
     """The kernel the bench's crypt call launches for S sessions (zrc4.hip
-    launch_crypt): at most WIN_MAX_GROUPS aligned groups -> 16 lanes per
-    stream (crypt_win_kernel); more 256-session groups than CUs -> the
-    persistent throughput kernel, otherwise one group per workgroup; grouped
-    ids always take crypt_kernel<kGrouped>."""
-    if ids == "grouped":
-        return "zrc4::crypt_kernel<2, false>"
+    launch_crypt): at most WIN_MAX_GROUPS groups (range batches from an
+    aligned first slot, or grouped buckets) -> 16 lanes per stream
+    (crypt_win_kernel); 2G <= CUs -> half-group workgroups; G <= CUs -> one
+    group per workgroup; more groups than CUs -> the persistent throughput
+    kernel (grouped buckets: its grouped form).  Scattered ids run the
+    per-lane gather forms."""
     try:
         import torch
         cus = torch.cuda.get_device_properties(0).multi_processor_count
     except Exception:
         cus = 256
     groups = -(-S // 256)
-    if ids == "range" and groups <= WIN_MAX_GROUPS:
-        return "zrc4::crypt_win_kernel"
-    if ids == "range" and 2 * groups <= cus:
-        return "zrc4::crypt_half_kernel<false>"
+    mode = {"range": 1, "grouped": 2, "scattered": 0}[ids]
     if ids == "scattered":
-        return "zrc4::crypt_stream_kernel<false>" if groups > cus else "zrc4::crypt_kernel<0, false>"
-    return "zrc4::crypt_stream_kernel<true>" if groups > cus else "zrc4::crypt_kernel<1, false>"
+        return "zrc4::crypt_stream_kernel<false, false>" if groups > cus else "zrc4::crypt_kernel<0, false>"
+    if groups <= WIN_MAX_GROUPS:
+        return f"zrc4::crypt_win_kernel<{mode}, false>"
+    if 2 * groups <= cus:
+        return f"zrc4::crypt_half_kernel<{mode}, false>"
+    if groups <= cus:
+        return f"zrc4::crypt_kernel<{mode}, false>"
+    return "zrc4::crypt_stream_kernel<true, true>" if ids == "grouped" else "zrc4::crypt_stream_kernel<true, false>"
 
 
 def load_traffic(workload: str):

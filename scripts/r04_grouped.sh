@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 4: grouped buckets on the persistent kernel -- parity, then same-process
+# A/B against the previous commit (old) for grouped and range batches.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r04/${R04_TAG:-grp}
+mkdir -p $OUT
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+step() {  # name, seconds, command...
+    local name=$1 secs=$2; shift 2
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "[$name] rc=$rc"; grep -v amdgpu.ids "$OUT/$name.log" | tail -${TAILN:-3} | cut -c1-1500
+    if [ $rc -ne 0 ]; then echo "[$name] failed: stopping GPU work in this call"; exit $rc; fi
+}
+TAILN=6 step tests 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+    -p no:cacheprovider -k "${R04_K:-grouped or staged or dispatch or window or baseline}"
+step ab_grouped 600 python tools/ab_bench.py --variant new: --variant old@HEAD: --ids grouped \
+    --workloads cfg5,262144x1024,cfg2,cfg3 --rounds 5 --launches 20
+step ab_range 600 python tools/ab_bench.py --variant new: --variant old@HEAD: \
+    --workloads cfg5,cfg2 --rounds 5 --launches 20
+echo r04 grouped done

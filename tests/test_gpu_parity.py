@@ -507,21 +507,27 @@ def grouped_batch(rng, n_groups, groups_total, fill=(1, 256)):
     return ids
 
 
-@pytest.mark.parametrize("fill,nb,trunc", [((256, 256), 64, 0), ((1, 256), 64, 0), ((1, 256), 200, 0),
-                                           ((1, 200), 64, 100), ((1, 256), 200, 37), ((1, 256), 27, 11)])
-def test_grouped_ids_bit_exact(built, torch_cuda, fill, nb, trunc):
+@pytest.mark.parametrize("fill,nb,trunc,idle", [
+    ((256, 256), 64, 0, 0), ((1, 256), 64, 0, 0), ((1, 256), 200, 0, 0),
+    ((1, 200), 64, 100, 0), ((1, 256), 200, 37, 0), ((1, 256), 27, 11, 0),
+    # more buckets than CUs: the persistent kernel's grouped form
+    ((1, 256), 600, 0, 0.1), ((256, 256), 1100, 0, 0), ((1, 200), 700, 100, 0.05), ((1, 64), 513, 255, 0.3)])
+def test_grouped_ids_bit_exact(built, torch_cuda, fill, nb, trunc, idle):
     """zrc4_crypt_grouped: each bucket a subset of ONE group, in any order,
     groups in random order, idle padding; two calls in a row continue the
     keystream.  nb = 27 buckets runs the speculative-window kernel (at most 32
     buckets, workgroup columns spread over the XCDs: 27 is no multiple of 8),
-    64 half-group workgroups, 200 whole-group ones; trunc drops the last entries of the batch (a short last bucket whose
-    slots still fall in both halves of its group).  Checked against the
-    oracle, every session that ran and every state; slots outside the batch
-    keep their state."""
+    64 half-group workgroups, 200 whole-group ones, 513-1 100 the persistent
+    kernel (2 workgroups per CU walking 1-3 buckets each: tables built a
+    bucket ahead, claims, gathered entries); trunc drops the last entries of
+    the batch (a short last bucket whose slots still fall in both halves of
+    its group); idle empties that share of the buckets (all ZRC4_IDLE_SLOT).
+    Checked against the oracle, every session that ran and every state;
+    slots outside the batch keep their state."""
     torch = torch_cuda
     from zsummerx_amd._capi import IDLE_SLOT
     rng = np.random.default_rng(41 + fill[0] + nb + trunc)
-    G = 256                                        # groups in the arena
+    G = max(256, nb + 64)                          # groups in the arena
     cap = 256 * G
     keys = rng.integers(0, 256, 16 * cap, dtype=np.uint8)
     koff = np.arange(cap, dtype=np.uint64) * 16
@@ -535,6 +541,9 @@ def test_grouped_ids_bit_exact(built, torch_cuda, fill, nb, trunc):
         touched = set()
         for call in range(2):
             ids = grouped_batch(rng, nb, G, fill)
+            if idle:
+                for b in np.flatnonzero(rng.random(nb - 1) < idle):
+                    ids[256 * b: 256 * (b + 1)] = IDLE_SLOT
             if trunc:   # the short bucket keeps an upper-half slot of its group (entry 0)
                 last = ids[256 * (nb - 1):]
                 used = [int(v) for v in last[last != IDLE_SLOT]]
@@ -597,7 +606,7 @@ def test_grouped_ids_mixed_bucket_is_refused(built, torch_cuda):
         assert got[256 * 32: 257 * 32].tobytes() == ks
 
 
-@pytest.mark.parametrize("nb", [20, 100, 200])
+@pytest.mark.parametrize("nb", [20, 100, 200, 700])
 def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb):
     """The cross-bucket half of the zrc4_crypt_grouped contract: two buckets
     of one call name the same group (disjoint slots of it).  The call reports
@@ -605,11 +614,12 @@ def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb):
     the contested group every entry is all-or-nothing -- crypted exactly as
     the oracle does with its state advanced, or untouched with its state
     unchanged -- never raced.  nb = 20: the window kernel (one claim per
-    dword column), 100: half-group workgroups, 200: whole-group workgroups."""
+    dword column), 100: half-group workgroups, 200: whole-group workgroups,
+    700: the persistent kernel (one claim per bucket, taken a group ahead)."""
     torch = torch_cuda
     from zsummerx_amd._capi import IDLE_SLOT
     rng = np.random.default_rng(500 + nb)
-    G = 256
+    G = max(256, nb + 8)
     cap = 256 * G
     keys = rng.integers(0, 256, 16 * cap, dtype=np.uint8)
     koff = np.arange(cap, dtype=np.uint64) * 16
@@ -667,6 +677,90 @@ def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb):
                 pyoracle.C.memmove(pyoracle.C.byref(st), saved, pyoracle.C.sizeof(st))
                 untouched += 1
         assert untouched >= 1 and crypted + untouched == 256
+
+
+def test_grouped_stream_refusals(built, torch_cuda):
+    """The persistent kernel's grouped form (600 buckets > 256 CUs) with every
+    refusal at once: a bucket whose busy entries span two groups, a bucket
+    naming one slot twice, a bucket with an id past the arena (that entry is
+    skipped, ZRC4_ERR_SLOT_RANGE, the rest of the bucket runs), idle buckets,
+    and a slot listed twice with length 0 once (not busy: allowed).  The call
+    reports ZRC4_ERR_GROUP; refused buckets leave payload and states
+    untouched; every other entry is bit-exact against the oracle.  A second
+    call afterwards (no faults) continues every keystream."""
+    torch = torch_cuda
+    from zsummerx_amd._capi import IDLE_SLOT
+    rng = np.random.default_rng(77)
+    nb = 600
+    G = nb + 64
+    cap = 256 * G
+    keys = rng.integers(0, 256, 16 * cap, dtype=np.uint8)
+    koff = np.arange(cap, dtype=np.uint64) * 16
+    klen = np.full(cap, 16, dtype=np.uint32)
+    ob = pyoracle.Batch(cap)
+    ob.make_sbox(keys, koff, klen)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    s = torch.cuda.current_stream()
+    mixed, twice, past, zero_dup = 5, 301, 450, 77
+    with Context(0, cap) as c:
+        c.ksa_range(0, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
+        for call in range(2):
+            ids = grouped_batch(rng, nb, G, (2, 256))
+            for b in (13, 14, 299, 599):
+                ids[256 * b: 256 * (b + 1)] = IDLE_SLOT
+            refused = set()
+            if call == 0:
+                bm = ids[256 * mixed: 256 * (mixed + 1)]
+                k = int(np.flatnonzero(bm != IDLE_SLOT)[0])
+                other = int(ids[256 * 7 + int(np.flatnonzero(ids[256 * 7: 256 * 8] != IDLE_SLOT)[0])])
+                spare = next(v for v in range((other // 256) * 256, (other // 256 + 1) * 256) if v not in set(ids.tolist()))
+                free = [p for p in range(256) if bm[p] == IDLE_SLOT] or [k ^ 1]
+                bm[free[0]] = spare                       # a slot of another bucket's group
+                bt = ids[256 * twice: 256 * (twice + 1)]
+                used = np.flatnonzero(bt != IDLE_SLOT)
+                dst = [p for p in range(256) if bt[p] == IDLE_SLOT]
+                bt[dst[0]] = bt[used[0]]                  # the same slot twice
+                refused = {mixed, twice}
+                bp = ids[256 * past: 256 * (past + 1)]
+                pos = [p for p in range(256) if bp[p] == IDLE_SLOT][0]
+                bp[pos] = cap + 1000                      # past the arena: skipped, bucket runs
+            bz = ids[256 * zero_dup: 256 * (zero_dup + 1)]
+            u = np.flatnonzero(bz != IDLE_SLOT)
+            zpos = [p for p in range(256) if bz[p] == IDLE_SLOT][0]
+            bz[zpos] = bz[u[0]]                           # listed twice, once with length 0
+            busy = (ids != IDLE_SLOT) & (ids < cap)
+            L = np.where(busy, rng.integers(1, 680, ids.size), 0).astype(np.uint32)
+            L[256 * zero_dup + zpos] = 0
+            busy &= L > 0
+            off = np.arange(ids.size, dtype=np.uint64) * 704 + rng.integers(0, 16, ids.size).astype(np.uint64)
+            data = rng.integers(0, 256, ids.size * 704 + 64, dtype=np.uint8)
+            want = data.copy()
+            before = {}
+            for e in np.flatnonzero(busy):
+                if e // 256 in refused:
+                    before[int(ids[e])] = ob.state(int(ids[e]))
+                    continue
+                st = ob.st[int(ids[e])]
+                pyoracle.lib().oracle_encryption(pyoracle.C.byref(st),
+                                                 pyoracle.C.c_void_p(want.ctypes.data + int(off[e])), int(L[e]))
+            pay = T(data)
+            c.crypt_grouped(pay, T(off.view(np.int64)), T(L.view(np.int32)), T(ids.view(np.int32)), stream=s)
+            if call == 0:
+                with pytest.raises(ZRC4Error) as ei:
+                    c.sync(s)
+                assert ei.value.code == -7                # ZRC4_ERR_GROUP (reported before SLOT_RANGE)
+            else:
+                c.sync(s)
+            got = pay.cpu().numpy()
+            bad = np.flatnonzero(got != want)
+            assert bad.size == 0, (call, bad[:8], int(bad.size), sorted({int(b) // 704 // 256 for b in bad[:50]}))
+            for slot, st0 in list(before.items())[:30]:
+                sb, x, y = c.get_state(slot)
+                assert (sb, x, y) == (bytes(st0[0]), st0[1], st0[2]), slot
+        for slot in [int(v) for v in ids[busy][:40]]:
+            sb, x, y = c.get_state(slot)
+            want_sb, wx, wy = ob.state(slot)
+            assert (sb, x, y) == (bytes(want_sb), wx, wy), slot
 
 
 # ------------------------------------------------ full BASELINE-size configs

@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--segment", action="store_true",
                     help="time each round's launches as one back-to-back segment (per-launch average)")
     ap.add_argument("--no-check", action="store_true", help="timing-only ablation builds (outputs differ)")
+    ap.add_argument("--ids", choices=["range", "grouped"], default="range",
+                    help="grouped: zrc4_crypt_grouped over the same batches with slots permuted inside each "
+                         "group and groups in random order (bench.py --ids grouped)")
     args = ap.parse_args()
 
     from zsummerx_amd import build
@@ -93,6 +96,30 @@ def main():
         ln = torch.full((n,), L, dtype=torch.int32, device=dev)
         scratch = torch.zeros(1000, dtype=torch.uint8, device=dev)
         zoff = torch.zeros(n, dtype=torch.int64, device=dev)
+        gids = None
+        if args.ids == "grouped":
+            # entry e of batch b -> session perm[e] (its slot, key, state and payload)
+            rng = np.random.default_rng(77)
+            perm = np.empty(n, dtype=np.int64)
+            for b in range(R):
+                Gs = -(-S // 256)
+                pos = 0
+                for g in rng.permutation(Gs):
+                    lo, hi = b * S + g * 256, min(b * S + (g + 1) * 256, (b + 1) * S)
+                    perm[b * S + pos: b * S + pos + (hi - lo)] = lo + rng.permutation(hi - lo)
+                    pos += hi - lo
+            gids = torch.from_numpy(perm.astype(np.int32)).to(dev)
+            off = torch.from_numpy(perm * L).to(dev)
+
+        def crypt(lib, h, b, buf=None):
+            if gids is None:
+                return lib.zrc4_crypt_range(h, b * S, C.c_void_p((pay if buf is None else buf).data_ptr()),
+                                            C.c_void_p(off.data_ptr() + 8 * b * S),
+                                            C.c_void_p(ln.data_ptr() + 4 * b * S), S, st)
+            return lib.zrc4_crypt_grouped(h, C.c_void_p(gids.data_ptr() + 4 * b * S),
+                                          C.c_void_p((pay if buf is None else buf).data_ptr()),
+                                          C.c_void_p(off.data_ptr() + 8 * b * S),
+                                          C.c_void_p(ln.data_ptr() + 4 * b * S), S, st)
         ctxs = []
         for name, lib in libs:
             h = C.c_void_p()
@@ -107,8 +134,7 @@ def main():
         ref = None
         for (name, lib), h in zip(libs, ctxs):
             buf = pay[: S * L].clone()
-            _capi.check(lib.zrc4_crypt_range(h, 0, C.c_void_p(buf.data_ptr()), C.c_void_p(off.data_ptr()),
-                                             C.c_void_p(ln.data_ptr()), S, st))
+            _capi.check(crypt(lib, h, 0, buf))
             _capi.check(lib.zrc4_sync(h, st))
             if ref is None:
                 ref = buf
@@ -145,9 +171,7 @@ def main():
                     if not args.segment:
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record(stream)
-                    rc = lib.zrc4_crypt_range(h, b * S, C.c_void_p(pay.data_ptr()),
-                                              C.c_void_p(off.data_ptr() + 8 * b * S),
-                                              C.c_void_p(ln.data_ptr() + 4 * b * S), S, st)
+                    rc = crypt(lib, h, b)
                     if not args.segment:
                         e1.record(stream)
                         evs.append((e0, e1))
@@ -167,7 +191,7 @@ def main():
         print(wl, json.dumps(report[wl]), flush=True)
         for (name, lib), h in zip(libs, ctxs):
             lib.zrc4_destroy(h)
-        del keys, adv, pay, off, ln, klen, koff, zoff
+        del keys, adv, pay, off, ln, klen, koff, zoff, gids
         torch.cuda.empty_cache()
     print(json.dumps(report))
 

@@ -124,7 +124,7 @@ def zl_block(base: int) -> str:
     return "ZL_BLOCK(" + ", ".join(f"v{base + d}" for d in range(16)) + ")"
 
 
-def half(name: str, cur: int, ab: int = 0) -> str:
+def half(name: str, cur: int, ab: int = 0, last: bool = False) -> str:
     """ab (timing-only A/B builds, zrc4_line_loop_ab.inc; outputs are wrong):
     1 stores to the lane's sink slot (one 64 KiB sink for the whole chip:
     contended), 2 loads from it, 3 no transpose, 4 both sinks.  (r02's 5 / 6,
@@ -144,12 +144,22 @@ def half(name: str, cur: int, ab: int = 0) -> str:
     # the previous half's stores (8) and loads (8) -> vmcnt(20).  Halves whose
     # line-after-next does not exist issue no loads, so the LAST half has
     # only 12 younger ops: it waits vmcnt(8) (both blocks) instead.
-    w(q("s_add_u32 %[s1], %[sb], 2"))
-    w(q("s_cmp_ge_u32 %[s1], %[wmax]"))
-    w(q(f"s_cbranch_scc0 LL_{name}W_%="))
-    w(q("s_waitcnt vmcnt(8)"))
-    w(q(f"LL_{name}W_%=:"))
-    w(q("s_waitcnt vmcnt(20)"))
+    # last (crypt_last_half_next_asm): the message's last half.  Its
+    # previous half never loads (no line after this one), so the wait is
+    # vmcnt(8) unconditionally -- the count the branch below always picks
+    # there -- and section 5 (loads of a line after this one) is absent, so
+    # every load this statement leaves is one the statement itself waits for
+    # (checkable without the relation between sb and wmax,
+    # tools/vmem_hazard_check.py).
+    if last:
+        w(q("s_waitcnt vmcnt(8)"))
+    else:
+        w(q("s_add_u32 %[s1], %[sb], 2"))
+        w(q("s_cmp_ge_u32 %[s1], %[wmax]"))
+        w(q(f"s_cbranch_scc0 LL_{name}W_%="))
+        w(q("s_waitcnt vmcnt(8)"))
+        w(q(f"LL_{name}W_%=:"))
+        w(q("s_waitcnt vmcnt(20)"))
     if name == "P":
         # entry of the first half: line 0 (P) was retired by the caller and
         # line 1 (Q) may still be in flight (issued after the S-box fill)
@@ -183,10 +193,20 @@ def half(name: str, cur: int, ab: int = 0) -> str:
         w(q(f"v_cndmask_b32_e64 v{sa + 1}, v{SINK + 1}, v{a + 1}, %[msk]"))
         if ab in (1, 4):
             sa = SINK
+        if ab == 5:
+            # the round-2 "sink load in place of each store" ablation that
+            # faulted the GPU in round 3: the load lands in the store-address
+            # temporaries asynchronously (--hazard-demo only: never built into
+            # a library that runs; tests/test_vmem_hazards.py checks that
+            # tools/vmem_hazard_check.py flags it)
+            w(f'"global_load_dwordx2 v[{sa}:{sa + 1}], v[{SINK}:{SINK + 1}], off\\n\\t"')
+            continue
         w(f'"global_store_dwordx4 v[{sa}:{sa + 1}], v[{final[qq]}:{final[qq] + 3}], off nt\\n\\t"')
     for qq in range(8):
         a = ADDR_BASE + 2 * qq
         w(q(f"v_lshl_add_u64 v[{a}:{a + 1}], 8, 4, v[{a}:{a + 1}]"))     # += 8 << 4 (shift must be 0..4)
+    if last:
+        return f"#define ZRC4_LL_HALF_{name}F \\\n    " + " \\\n    ".join(out) + "\n"
     # 5. loads of the line two halves ahead (blocks b+4, b+5) into this set;
     #    palo:pahi = own payload + 64 * (b + 4) on entry
     w(q("s_add_u32 %[s1], %[sb], 4"))
@@ -239,10 +259,24 @@ def main(ab_only: bool = False):
         "#pragma once\n",
         half("P", P_BASE),
         half("Q", Q_BASE),
+        half("Q", Q_BASE, last=True),
         transpose_only("P", P_BASE),
     ]
     OUT.write_text("".join(text))
     print("wrote", OUT)
+
+
+def write_hazard_demo(out_dir: Path) -> Path:
+    """The removed round-2 ablation 5 as THE line loop, into a scratch dir
+    (tests/test_vmem_hazards.py builds it next to copies of the kernels and
+    expects tools/vmem_hazard_check.py to flag it).  Never run on a GPU."""
+    out_dir.mkdir(parents=True, exist_ok=True)
+    text = ["// GENERATED by tools/gen_line_loop.py --hazard-demo: BROKEN on purpose (never run it).\n",
+            "#pragma once\n", half("P", P_BASE, 5), half("Q", Q_BASE, 5), half("Q", Q_BASE, 5, last=True),
+            transpose_only("P", P_BASE)]
+    out = out_dir / "zrc4_line_loop.inc"
+    out.write_text("".join(text))
+    return out
 
 
 def write_ab():
@@ -260,4 +294,7 @@ def write_ab():
 
 
 if __name__ == "__main__":
-    main(ab_only="--ab" in sys.argv[1:])
+    if "--hazard-demo" in sys.argv[1:]:
+        print("wrote", write_hazard_demo(Path(sys.argv[sys.argv.index("--hazard-demo") + 1])))
+    else:
+        main(ab_only="--ab" in sys.argv[1:])

@@ -95,7 +95,7 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
 {
     if (n == 0) return ZRC4_OK;
     if (mode == zrc4::kRange && (uint64_t)first_slot + n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
-    zrc4::Claim cl{nullptr, 0u};
+    zrc4::Claim cl{nullptr, 0u, nullptr};
     if (mode == zrc4::kGrouped) {
         // a fresh tag per grouped launch; on the 32-bit wrap the words are
         // zeroed first (stream-ordered before this launch)
@@ -103,11 +103,15 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
             ZRC4_TRY(hipMemsetAsync(c->claim, 0, (size_t)(c->capacity / zrc4::kGroup) * zrc4::kClaimParts * 8u, s));
             c->epoch = 1u;
         }
-        cl = zrc4::Claim{c->claim, c->epoch};
+        cl = zrc4::Claim{c->claim, c->epoch,
+                         reinterpret_cast<const uint32_t *>(c->claim + (size_t)(c->capacity / zrc4::kGroup) * zrc4::kClaimParts)};
     }
     const uint32_t grid = (n + zrc4::kGroup - 1) / zrc4::kGroup;
     const dim3 blk(zrc4::kGroup);
-    const bool stream_kernel = mode != zrc4::kGrouped && grid > (uint32_t)c->num_cus;
+    const bool stream_kernel = grid > (uint32_t)c->num_cus;
+    // (the grouped stream kernel computes entry indexes of the bucket after
+    // next in 32 bits)
+    if (mode == zrc4::kGrouped && stream_kernel && n > 0xFFF00000u) return ZRC4_ERR_INVALID_ARG;
     // Few aligned groups: 16 lanes per stream (speculative windows), one wave
     // per 4 streams, 64 workgroups per group.
     if (grid <= (uint32_t)ZRC4_WIN_MAX_GROUPS &&
@@ -174,12 +178,15 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
     }
     if (stream_kernel) {
         const uint32_t wgs = std::min(grid, 2u * (uint32_t)c->num_cus);
-        if (mode == zrc4::kRange && (first_slot & 255u) == 0u)
-            hipLaunchKernelGGL(zrc4::crypt_stream_kernel<true>, dim3(wgs), blk, 0, s, c->arena, c->xy, ids,
-                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
+        if (mode == zrc4::kGrouped)
+            hipLaunchKernelGGL((zrc4::crypt_stream_kernel<true, true>), dim3(wgs), blk, 0, s, c->arena, c->xy, ids,
+                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink, cl);
+        else if (mode == zrc4::kRange && (first_slot & 255u) == 0u)
+            hipLaunchKernelGGL((zrc4::crypt_stream_kernel<true, false>), dim3(wgs), blk, 0, s, c->arena, c->xy, ids,
+                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink, cl);
         else
-            hipLaunchKernelGGL(zrc4::crypt_stream_kernel<false>, dim3(wgs), blk, 0, s, c->arena, c->xy, ids,
-                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
+            hipLaunchKernelGGL((zrc4::crypt_stream_kernel<false, false>), dim3(wgs), blk, 0, s, c->arena, c->xy,
+                               ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, cl);
     } else if (mode == zrc4::kRange) {
         hipLaunchKernelGGL(zrc4::crypt_kernel<zrc4::kRange>, dim3(grid), blk, 0, s, c->arena, c->xy, ids,
                            first_slot, payload, off, len, n, c->capacity, c->err, c->sink);
@@ -252,8 +259,9 @@ int zrc4_create(zrc4_ctx **out, int device, uint32_t capacity)
               hipMalloc(&c->xy, (size_t)c->capacity * sizeof(uint16_t)) == hipSuccess &&
               hipMalloc(&c->sink, zrc4::kSinkBytes) == hipSuccess &&
               hipHostMalloc(&c->err, zrc4::kErrWords * sizeof(uint32_t), hipHostMallocCoherent) == hipSuccess &&
-              hipMalloc(&c->claim, groups * zrc4::kClaimParts * sizeof(unsigned long long)) == hipSuccess &&
-              hipMemset(c->claim, 0, groups * zrc4::kClaimParts * sizeof(unsigned long long)) == hipSuccess &&
+              // + 16 zero bytes after the claim words (Claim::zero; the epoch-wrap memset stops before them)
+              hipMalloc(&c->claim, (groups * zrc4::kClaimParts + 2) * sizeof(unsigned long long)) == hipSuccess &&
+              hipMemset(c->claim, 0, (groups * zrc4::kClaimParts + 2) * sizeof(unsigned long long)) == hipSuccess &&
               hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     if (!ok) { zrc4_destroy(c); return ZRC4_ERR_OUT_OF_MEMORY; }
     // Fresh slots hold the reference's empty-key state: identity box, x = y = 0

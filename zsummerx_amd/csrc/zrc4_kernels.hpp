@@ -68,6 +68,7 @@ constexpr uint32_t kClaimParts = 64;
 struct Claim {
     unsigned long long *word;   // [groups][kClaimParts]
     uint32_t epoch;
+    const uint32_t *zero;       // 16 zero bytes (crypt_stream_kernel<true, true>: the entry of an idle lane)
 };
 
 __device__ __forceinline__ unsigned long long claim_part(const Claim &cl, uint32_t g, uint32_t part,
@@ -753,7 +754,7 @@ __device__ __forceinline__ void crypt_last_half_next_asm(Rc4Lane &st, u32x32 &P,
     asm volatile(
         "s_mov_b64 %[full], exec\n\t"
         ZRC4_NEXT_LINE0
-        ZRC4_LL_HALF_Q
+        ZRC4_LL_HALF_QF
         "LL_DONE_%=:\n\t"
         "s_mov_b64 exec, %[full]\n\t"
         "s_waitcnt vmcnt(8)\n\t"             // the next line 0 (only this half's 8 stores are younger)
@@ -1402,6 +1403,169 @@ __device__ __forceinline__ void prefetch_group(u32x32 &P, u32x32 &Q, u32x32 &ilo
 }
 
 
+// ---------------------------------------------------------------------------
+// Grouped batches in the persistent kernel (crypt_stream_kernel<true, true>,
+// zrc4_crypt_grouped with more buckets than CUs).  Bucket b holds entries
+// b*256 .. b*256+255; its busy entries (a slot id < capacity, length > 0) must
+// name ONE group, no slot twice, and no other bucket of the call may name that
+// group (include/zrc4.h).  Lane j of the workgroup runs slot g*256 + j, so the
+// image moves as one coalesced copy and the LDS columns stay conflict-free.
+//
+// Pipeline (one group per ~57 us of keystream at 1 KiB): while bucket n runs,
+//   * bucket n+1's image, x/y (slot order: g*256 + j), its permuted entries
+//     (this lane's length and offset, gathered by the entry index its table
+//     names) and its claim are in flight -- exactly the range kernel's
+//     prefetch plus one claim -- and
+//   * bucket n+2's raw ids and lengths (entry order) are in flight.
+// At the boundary into bucket n+1 (in the LDS fill of its image) the raw ids
+// of bucket n+2 build its slot -> entry table in LDS; after the fill barrier
+// each lane reads its entry and the four waves' group votes, so bucket n+2's
+// image address is known a whole group before its keystream starts.  The
+// table and the votes are tagged with the bucket (an entry index e belongs
+// to bucket e >> 8), so nothing is cleared between buckets.
+//
+// LDS (after the 64 KiB image at offset 0): 64 B of votes -- per wave its
+// group guess (first busy id's group, or ZRC4_INVALID) and a bad word
+// (another group or a slot twice) -- plus the claim-lost word, then the
+// 256-word table slot & 255 -> entry index.
+// Word offsets from gr = smem + kGroupBytes (one base register for all of them).
+constexpr uint32_t kGrVote = 0;                          // 4 waves x {guess, bad}
+constexpr uint32_t kGrLost = 8;                          // the current bucket's claim was lost
+constexpr uint32_t kGrTab = 16;                          // slot & 255 -> entry index
+constexpr uint32_t kSmemStreamGr = kGroupBytes + 4u * (kGrTab + 256u);   // 66 624 B: two workgroups per CU
+
+// The table of bucket nb from its raw entries (thread j holds entry nb*256 +
+// j), plus this wave's vote.  Call between two barriers that order it after
+// every read of the previous table.
+__device__ __forceinline__ void bucket_table(uint32_t *gr, uint32_t nb, uint32_t id, uint32_t ln, uint32_t n,
+                                             uint32_t capacity, uint32_t *err)
+{
+    const uint32_t j = threadIdx.x, e = nb * kGroup + j;
+    const bool v = e < n;
+    if (v && id >= capacity && id != ZRC4_INVALID) {        // ZRC4_IDLE_SLOT pads buckets
+        latch_fault(err, kErrSlotRange);
+        id = ZRC4_INVALID;
+    }
+    const bool busy = v && id != ZRC4_INVALID && ln != 0u;
+    const uint64_t bm = __ballot(busy);
+    const uint32_t guess = bm ? __builtin_amdgcn_readlane(id, (int)__builtin_ctzll(bm)) >> 8 : ZRC4_INVALID;
+    const uint32_t old = busy ? atomicExch(&gr[kGrTab + (id & 255u)], e) : ZRC4_INVALID;
+    const bool bad = __ballot(busy && ((id >> 8) != guess || (old >> 8) == nb)) != 0u;
+    if ((j & 63u) == 0u) {
+        const uint32_t wv = __builtin_amdgcn_readfirstlane(j >> 6);   // (an SGPR: no VGPR held across the loop)
+        gr[kGrVote + 2u * wv] = guess;
+        gr[kGrVote + 2u * wv + 1u] = bad ? 1u : 0u;
+    }
+}
+
+struct BucketView {
+    uint32_t g;      // the bucket's group (0 when idle or refused: an in-bounds address)
+    uint32_t ent;    // this lane's entry (valid) or the bucket's first entry
+    bool ok;         // busy entries, one group, no slot twice (wave-uniform)
+    bool valid;      // this lane's slot g*256 + j has an entry
+};
+
+// After the barrier that follows bucket_table(nb): the votes and this lane's
+// table entry.  A refused bucket latches kErrGroup (thread 0).
+__device__ __forceinline__ BucketView bucket_read(const uint32_t *gr, uint32_t nb, uint32_t *err)
+{
+    const uint4 va = *reinterpret_cast<const uint4 *>(gr + kGrVote), vb = *reinterpret_cast<const uint4 *>(gr + kGrVote + 4);
+    const uint32_t vote[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+    uint32_t g = ZRC4_INVALID;
+    bool bad = false;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t gw = __builtin_amdgcn_readfirstlane(vote[2 * w]);
+        bad = bad || __builtin_amdgcn_readfirstlane(vote[2 * w + 1]) != 0u;
+        if (gw != ZRC4_INVALID) {
+            if (g == ZRC4_INVALID) g = gw;
+            else if (gw != g) bad = true;
+        }
+    }
+    BucketView bv;
+    bv.ok = g != ZRC4_INVALID && !bad;
+    if (g != ZRC4_INVALID && bad && threadIdx.x == 0u) latch_fault(err, kErrGroup);
+    const uint32_t t = gr[kGrTab + threadIdx.x];
+    bv.valid = bv.ok && (t >> 8) == nb;
+    bv.g = bv.ok ? g : 0u;
+    bv.ent = bv.valid ? t : nb * kGroup;
+    return bv;
+}
+
+// The next bucket's claim (lane 0 of wave 0 swaps the launch epoch into the
+// high half of the group's part-0 claim word -- only the epoch decides a
+// claim -- and every other wave reads that half instead, so every wave issues
+// the same number of VMEM ops and the counted waits hold), its permuted entry
+// (an idle lane reads zeros), x/y, the raw ids and lengths of the bucket after
+// it, and its image -- in that order, from asm (see prefetch_group).
+// Consumers wait:
+//   claim, entries, raw  "s_waitcnt vmcnt(16)" (the 16 image loads are younger);
+//   image                "s_waitcnt vmcnt(24)".
+__device__ __forceinline__ void prefetch_bucket(u32x32 &P, u32x32 &Q, u32x32 &ilo, u32x32 &ihi, uint32_t &cold,
+                                                uint32_t &rlen, uint64_t &roff, uint32_t &rxy, uint32_t &qid,
+                                                uint32_t &qlen, const uint32_t *cw, uint32_t cv,
+                                                uint32_t doclaim, const uint32_t *alen, const uint64_t *aoff,
+                                                const uint16_t *axy, const uint32_t *aqid, const uint32_t *aqlen,
+                                                const uint8_t *ibase, uint32_t j)
+{
+    uint32_t vo;
+    uint64_t sv;
+    asm volatile(
+        "s_mov_b64 %[sv], exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "s_cmp_eq_u32 %[dc], 0\n\t"
+        "s_cbranch_scc1 PB_READ_%=\n\t"
+        "global_atomic_swap %[cold], %[cw], %[cv], off sc0\n\t"
+        "s_branch PB_CLAIMED_%=\n\t"
+        "PB_READ_%=:\n\t"
+        "global_load_dword %[cold], %[cw], off\n\t"
+        "PB_CLAIMED_%=:\n\t"
+        "s_mov_b64 exec, %[sv]\n\t"
+        "global_load_dword %[rlen], %[alen], off\n\t"
+        "global_load_dwordx2 %[roff], %[aoff], off\n\t"
+        "global_load_ushort %[rxy], %[axy], off\n\t"
+        "global_load_dword %[qid], %[aqid], off\n\t"
+        "global_load_dword %[qlen], %[aqlen], off\n\t"
+        "v_lshlrev_b32 %[vo], 4, %[j]\n\t"
+        "global_load_dwordx4 v[160:163], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[164:167], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[168:171], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[172:175], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[176:179], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[180:183], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[184:187], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[188:191], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[192:195], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[196:199], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[200:203], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[204:207], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[208:211], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[212:215], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[216:219], %[vo], %[ib]\n\t"
+        "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
+        "global_load_dwordx4 v[220:223], %[vo], %[ib]\n\t"
+        : "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[160:191]}"(ilo), "=&{v[192:223]}"(ihi), [cold] "=&v"(cold),
+          [rlen] "=&v"(rlen), [roff] "=&v"(roff), [rxy] "=&v"(rxy), [qid] "=&v"(qid), [qlen] "=&v"(qlen),
+          [vo] "=&v"(vo), [sv] "=&s"(sv)
+        : [cw] "v"(cw), [cv] "v"(cv), [dc] "s"(doclaim), [alen] "v"(alen), [aoff] "v"(aoff), [axy] "v"(axy),
+          [aqid] "v"(aqid), [aqlen] "v"(aqlen), [ib] "s"(ibase), [j] "v"(j)
+        : "memory", "scc");
+}
+
 // crypt_stream_kernel's copy-out of a group's S-boxes at a group boundary:
 // all 16 LDS reads in flight at once, then the 16 stores (the compiler's
 // version paired them, one LDS round trip per pair, while the other
@@ -1467,17 +1631,19 @@ __device__ __forceinline__ void lds_to_image_asm(uint8_t *img, uint32_t tid)
         : "memory");
 }
 
-template <bool PF>
+template <bool PF, bool GR = false>
 __global__ void __launch_bounds__(256, 2)
 crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                     const uint32_t *__restrict__ ids, uint32_t first_slot,
                     uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
                     const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
-                    uint32_t *__restrict__ err, uint8_t *__restrict__ sink)
+                    uint32_t *__restrict__ err, uint8_t *__restrict__ sink, Claim cl = Claim{})
 {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kGroupBytes + 16];
+    static_assert(PF || !GR, "grouped batches run the prefetching form");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[GR ? kSmemStreamGr : kGroupBytes + 16];
     uint8_t *S = smem;
     if (!lds_base_ok(S, err)) return;
+    uint32_t *gr = reinterpret_cast<uint32_t *>(smem + kGroupBytes);    // GR: votes, claim word, table
     const uint32_t j = threadIdx.x;
     const uint32_t col = col_of(j);
     const uint32_t nwg = (n + kGroup - 1) / kGroup;
@@ -1488,10 +1654,43 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 
     uint32_t w = blockIdx.x;
     EntryIn cur;
-    load_entry(cur, w, j, ids, first_slot, off, len, n, capacity, err, xy);
+    // GR: this bucket's group and whether it runs (wave-uniform), its claim
+    // word's old value (lane 0 of wave 0), and the next bucket's raw entry.
+    uint32_t gcur = 0;
+    bool cur_ok = false;
+    uint32_t cold = 0;
+    uint32_t qid = ZRC4_INVALID, qlen = 0;
+    if constexpr (GR) {
+        // Prologue: bucket w's table (compiler loads, waited for once below),
+        // its claim, permuted entry, x/y and image; bucket w + grid's raw entry.
+        gr[kGrTab + j] = ZRC4_INVALID;
+        const uint32_t e0 = w * kGroup + j, e1 = (w + gridDim.x) * kGroup + j;
+        const uint32_t id0 = e0 < n ? ids[e0] : ZRC4_INVALID, l0 = e0 < n ? len[e0] : 0u;
+        if (e1 < n) {
+            qid = ids[e1];
+            qlen = len[e1];
+        }
+        __syncthreads();
+        bucket_table(gr, w, id0, l0, n, capacity, err);
+        __syncthreads();
+        const BucketView bv = bucket_read(gr, w, err);
+        gcur = bv.g;
+        cur_ok = bv.ok;
+        if (bv.ok && j == 0u)
+            cold = __hip_atomic_exchange(reinterpret_cast<uint32_t *>(cl.word + (size_t)bv.g * kClaimParts) + 1,
+                                         cl.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cur.len = bv.valid ? len[bv.ent] : 0u;
+        cur.off = bv.valid ? off[bv.ent] : 0u;
+        cur.slot = bv.valid ? bv.g * 256u + j : ZRC4_INVALID;
+        cur.xy = xy[bv.g * 256u + j];
+        __syncthreads();                      // table and votes read before the next bucket's are built
+    } else {
+        load_entry(cur, w, j, ids, first_slot, off, len, n, capacity, err, xy);
+    }
     u32x32 ilo, ihi;                          // PF: this group's image, 16 x 16 B per lane
     if constexpr (PF) {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(arena + (size_t)((first_slot >> 8) + w) * kGroupBytes);
+        const uint32_t g0 = GR ? gcur : (first_slot >> 8) + w;
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(arena + (size_t)g0 * kGroupBytes);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const u32x4 a = src[i * 256 + j], b = src[(i + 8) * 256 + j];
@@ -1512,15 +1711,15 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     // the asm prefetch -- into every iteration.
     asm volatile("" : "+v"(cur.len), "+v"(cur.off), "+v"(cur.xy), "+{v[40:71]}"(P),
                  "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi));
+    if constexpr (GR) asm volatile("" : "+v"(cold), "+v"(qid), "+v"(qlen));
 
     for (;;) {
         // ---- this group's S-boxes into LDS
         bool whole;
         uint32_t g;
-        const bool active = cur.slot != ZRC4_INVALID;
         if constexpr (PF) {
-            whole = true;
-            g = (first_slot >> 8) + w;
+            whole = GR ? cur_ok : true;
+            g = GR ? gcur : (first_slot >> 8) + w;
             // younger than the prefetched image: at least the next group's
             // line-0 loads (8) and this image's stores (16)
             asm volatile("s_waitcnt vmcnt(24)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
@@ -1530,8 +1729,27 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                 dst[i * 256 + j] = u32x4{ilo[4 * i], ilo[4 * i + 1], ilo[4 * i + 2], ilo[4 * i + 3]};
                 dst[(i + 8) * 256 + j] = u32x4{ihi[4 * i], ihi[4 * i + 1], ihi[4 * i + 2], ihi[4 * i + 3]};
             }
+            if constexpr (GR) {
+                // this bucket's claim (read back with the entries), and the
+                // table of the bucket after next from its raw entries
+                if (j == 0u) gr[kGrLost] = cur_ok && cold == cl.epoch ? 1u : 0u;
+                if (w + gridDim.x < nwg) bucket_table(gr, w + gridDim.x, qid, qlen, n, capacity, err);
+            }
             __syncthreads();
+            if constexpr (GR) {
+                const uint32_t lost = __builtin_amdgcn_readfirstlane(gr[kGrLost]);
+                if (cur_ok && lost != 0u) {
+                    // another bucket of this launch holds the group: skip this one whole
+                    if (j == 0u) latch_fault(err, kErrGroup);
+                    cur_ok = false;
+                    whole = false;
+                    cur.len = 0u;
+                    cur.slot = ZRC4_INVALID;
+                    line_setup(ls, payload, 0u);
+                }
+            }
         } else {
+            const bool act = cur.slot != ZRC4_INVALID;
             if (!ids) {
                 whole = (first_slot & 255u) == 0u;
                 g = (first_slot >> 8) + w;
@@ -1543,24 +1761,26 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                 volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(smem + kGroupBytes);
                 if (j == 0) flag[0] = 1u;
                 __syncthreads();
-                if (!(active && cur.slot == ((first & ~255u) + j) && (first & 255u) == 0u)) flag[0] = 0u;
+                if (!(act && cur.slot == ((first & ~255u) + j) && (first & 255u) == 0u)) flag[0] = 0u;
                 __syncthreads();
                 whole = flag[0] != 0u;
             }
             if (whole) {
                 image_to_lds(S, arena + (size_t)g * kGroupBytes);
                 __syncthreads();
-            } else if (active && cur.len) {
+            } else if (act && cur.len) {
                 gather_column(S, col, arena, cur.slot);
             }
         }
+        const bool active = cur.slot != ZRC4_INVALID;
 
         // ---- next group's entries and image, in flight during the keystream (PF)
         const uint32_t wn = w + gridDim.x;
         const bool more = wn < nwg;
         uint32_t rlen = 0, rxy = 0;
         uint64_t roff = 0;
-        uint32_t en = 0;
+        uint32_t en = 0, nvalid = 0, gn = 0;
+        bool nok = false;
         // This group's line 0 is needed now (compiler wait; the previous
         // image's stores are younger); past this point it is asm-defined, so
         // nothing the compiler tracks is pending at the loop.  Line 1 goes out
@@ -1568,10 +1788,25 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         asm volatile("" : "+{v[40:71]}"(P));
         p_async = false;
         if (ls.wmax > 2u) issue_line1_asm(Q, ls, sk);
-        if constexpr (PF) {
+        if constexpr (GR) {
+            if (more) {
+                const BucketView bv = bucket_read(gr, wn, err);
+                gn = bv.g;
+                nok = bv.ok;
+                const uint32_t eq = (wn + gridDim.x) * kGroup + j < n ? (wn + gridDim.x) * kGroup + j : n - 1u;
+                const uint32_t dc = __builtin_amdgcn_readfirstlane(nok && j < 64u ? 1u : 0u);
+                prefetch_bucket(P, Q, ilo, ihi, cold, rlen, roff, rxy, qid, qlen,
+                                reinterpret_cast<const uint32_t *>(cl.word + (size_t)gn * kClaimParts) + 1, cl.epoch,
+                                dc, bv.valid ? len + bv.ent : cl.zero,
+                                bv.valid ? off + bv.ent : reinterpret_cast<const uint64_t *>(cl.zero),
+                                xy + gn * 256u + j, ids + eq, len + eq, arena + (size_t)gn * kGroupBytes, j);
+                nvalid = 1u;                          // idle lanes read length 0
+            }
+        } else if constexpr (PF) {
             if (more) {
                 en = wn * kGroup + j;
                 const uint32_t ec = en < n ? en : n - 1u;          // in-bounds address for idle lanes
+                nvalid = en < n ? 1u : 0u;
                 prefetch_group(P, Q, ilo, ihi, rlen, roff, rxy, len + ec, off + ec, xy + first_slot + ec,
                                arena + (size_t)((first_slot >> 8) + wn) * kGroupBytes, j);
             }
@@ -1594,7 +1829,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             // Before the message's final half (even half counts) the next
             // group's line 0 goes into P (crypt_last_half_next_asm).
             p_async = crypt_message_dpp(S, st, payload + cur.off, cur.len, P, Q, ls, sk, PF && more, rlen, roff,
-                                        en < n ? 1u : 0u, payload);
+                                        nvalid, payload);
             if (active && cur.len) xy[cur.slot] = lane_xy(st);
         }
         stream_stamp(sink, 2u + 2u * k_t);
@@ -1605,13 +1840,23 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             if constexpr (PF) {
                 // (already waited for when line 0 went out early: a wait here
                 // would also wait for it)
-                if (!p_async)
-                    asm volatile("s_waitcnt vmcnt(16)" : "+v"(rlen), "+v"(roff), "+v"(rxy) :: "memory");
-                const bool v = en < n;
-                nxt.len = v ? rlen : 0u;
-                nxt.off = v ? roff : 0u;
-                nxt.slot = v ? first_slot + en : ZRC4_INVALID;
-                nxt.xy = v ? rxy : 0u;
+                if constexpr (GR) {
+                    if (!p_async)
+                        asm volatile("s_waitcnt vmcnt(16)"
+                                     : "+v"(rlen), "+v"(roff), "+v"(rxy), "+v"(cold), "+v"(qid), "+v"(qlen) :: "memory");
+                    nxt.len = rlen;           // 0 for lanes without an entry (and for idle / refused buckets)
+                    nxt.off = roff;
+                    nxt.slot = gn * 256u + j;
+                    nxt.xy = rxy;
+                } else {
+                    if (!p_async)
+                        asm volatile("s_waitcnt vmcnt(16)" : "+v"(rlen), "+v"(roff), "+v"(rxy) :: "memory");
+                    const bool v = nvalid != 0u;
+                    nxt.len = v ? rlen : 0u;
+                    nxt.off = v ? roff : 0u;
+                    nxt.slot = v ? first_slot + en : ZRC4_INVALID;
+                    nxt.xy = v ? rxy : 0u;
+                }
             } else {
                 load_entry(nxt, wn, j, ids, first_slot, off, len, n, capacity, err, xy);
             }
@@ -1624,13 +1869,20 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         if (whole) {
             __syncthreads();
             lds_to_image_asm(arena + (size_t)g * kGroupBytes, j);
-        } else if (active && cur.len) {
+        } else if (!PF && active && cur.len) {
             scatter_column(arena, cur.slot, S, col);
+        } else if (GR) {
+            // An idle or refused bucket stores no image, so the next fill's
+            // counted wait (16 image stores younger than the prefetched
+            // image) would not cover the image: retire everything here.
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         if (!more) break;
         __syncthreads();      // every wave has read this image out of LDS before the next fill
         cur = nxt;
         w = wn;
+        gcur = gn;
+        cur_ok = nok;
     }
 #if ZRC4_TIMING
     __builtin_amdgcn_s_waitcnt(0);

@@ -241,6 +241,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
     uint64_t O = 0;
     bool valid;
     uint32_t rows[4];
+    uint32_t sxy;
     if constexpr (MODE == kRange) {
         const uint32_t e = wg * kGroup + kb;
         ent = e;
@@ -255,6 +256,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             L = len[e];
             O = off[e];
         }
+        sxy = valid ? xy[slot] : 0u;
     } else {
         uint32_t *te = reinterpret_cast<uint32_t *>(Ring);                    // slot & 255 -> entry
         uint32_t *tl = te + 256;                                              // length
@@ -300,6 +302,8 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
+        // x/y of the stream on the same guess (no round trip after the table build)
+        const uint32_t sxy_g = xy[gw * 256u + kb];
         unsigned long long cold = 0;                                          // the claim of column q (Claim)
         if (lane == 0) cold = claim_part(cl, gw, q, wg);
         __syncthreads();
@@ -327,11 +331,11 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             L = tl[kb];
             O = to[kb];
         }
+        sxy = valid ? sxy_g : 0u;
         if (!__builtin_amdgcn_ballot_w64(valid)) return;
         __syncthreads();                                                      // tables read before the ring is used
     }
     uint8_t *img = arena + (size_t)(slot >> 8) * kGroupBytes + 4u * q;
-    const uint32_t sxy = valid ? xy[slot] : 0u;
     uint8_t *msg = payload + O;
     const bool aligned = ((uintptr_t)msg & 15u) == 0u;
 
