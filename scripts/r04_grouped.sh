@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4: grouped buckets on the persistent kernel -- parity, then same-process
-# A/B against the previous commit (old) for grouped and range batches.
+# A/B: new (this tree), l0c (next line 0 as compiler loads, ZRC4_LINE0_ASM=0)
+# and old (the round-3 tree, 4754ac6), for grouped and range batches.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/r04/${R04_TAG:-grp}
@@ -15,8 +16,7 @@ step() {  # name, seconds, command...
 }
 TAILN=6 step tests 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
     -p no:cacheprovider -k "${R04_K:-grouped or staged or dispatch or window or baseline}"
-step ab_grouped 600 python tools/ab_bench.py --variant new: --variant old@HEAD: --ids grouped \
-    --workloads cfg5,262144x1024,cfg2,cfg3 --rounds 5 --launches 20
-step ab_range 600 python tools/ab_bench.py --variant new: --variant old@HEAD: \
-    --workloads cfg5,cfg2 --rounds 5 --launches 20
+V="--variant new: --variant l0c:ZRC4_LINE0_ASM=0 --variant old@4754ac6:"
+step ab_grouped 600 python tools/ab_bench.py $V --ids grouped --workloads cfg5,262144x1024,cfg2,cfg3 --rounds 5 --launches 20
+step ab_range 600 python tools/ab_bench.py $V --workloads cfg5,262144x1024,131072x1024,cfg2 --rounds 5 --launches 20
 echo r04 grouped done

@@ -631,6 +631,33 @@ __device__ __forceinline__ void preload_line0(u32x32 &P, const LineSetup &ls, co
     preload_line(P, nb > 0 ? p : sk, nb > 1 ? p + 64 : sk + 64);
 }
 
+// Line 0 of the next group from asm (ZRC4_LINE0_ASM): issued after the
+// keystream, before the image copy-out, and waited for after the next fill
+// with a counted vmcnt(16) (the 16 image stores are the only younger VMEM
+// ops) -- as compiler loads, the compiler drains everything there
+// (vmcnt(0)), the image stores included.
+#ifndef ZRC4_LINE0_ASM
+#define ZRC4_LINE0_ASM 1
+#endif
+__device__ __forceinline__ void issue_line0_asm(u32x32 &P, const LineSetup &ls, const uint8_t *sk)
+{
+    const uint8_t *p = reinterpret_cast<const uint8_t *>((uintptr_t)ls.p);
+    const uint32_t nb = ls.nblk;
+    const uint8_t *b0 = nb > 0 ? p : sk, *b1 = nb > 1 ? p + 64 : sk + 64;
+    asm volatile(
+        "global_load_dwordx4 v[40:43], %[a0], off\n\t"
+        "global_load_dwordx4 v[44:47], %[a0], off offset:16\n\t"
+        "global_load_dwordx4 v[48:51], %[a0], off offset:32\n\t"
+        "global_load_dwordx4 v[52:55], %[a0], off offset:48\n\t"
+        "global_load_dwordx4 v[56:59], %[a1], off\n\t"
+        "global_load_dwordx4 v[60:63], %[a1], off offset:16\n\t"
+        "global_load_dwordx4 v[64:67], %[a1], off offset:32\n\t"
+        "global_load_dwordx4 v[68:71], %[a1], off offset:48\n\t"
+        : "=&{v[40:71]}"(P)
+        : [a0] "v"(b0), [a1] "v"(b1)
+        : "memory");
+}
+
 // Line 1 (blocks 2, 3), issued from asm after the S-box fill, so it is in
 // flight while line 0's keystream runs (the loop's first half is entered past
 // its wait; the second half's counted wait retires it).  Only when the wave
@@ -1785,7 +1812,14 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         // image's stores are younger); past this point it is asm-defined, so
         // nothing the compiler tracks is pending at the loop.  Line 1 goes out
         // now, behind the fill, and is waited for inside the loop.
+#if ZRC4_LINE0_ASM
+        if constexpr (PF)
+            asm volatile("s_waitcnt vmcnt(16)" : "+{v[40:71]}"(P) :: "memory");   // younger: the 16 image stores
+        else
+            asm volatile("" : "+{v[40:71]}"(P));
+#else
         asm volatile("" : "+{v[40:71]}"(P));
+#endif
         p_async = false;
         if (ls.wmax > 2u) issue_line1_asm(Q, ls, sk);
         if constexpr (GR) {
@@ -1862,7 +1896,14 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             }
             // the loop's last two halves issue no loads, so P/Q are free again
             line_setup(ls, payload + nxt.off, nxt.len);
-            if (!p_async) preload_line0(P, ls, sk);
+            if (!p_async) {
+#if ZRC4_LINE0_ASM
+                if constexpr (PF) issue_line0_asm(P, ls, sk);
+                else preload_line0(P, ls, sk);
+#else
+                preload_line0(P, ls, sk);
+#endif
+            }
         }
 
         // ---- this group's state back to HBM
