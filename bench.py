@@ -570,12 +570,17 @@ def ksa_storm(args):
     import torch
     from zsummerx_amd import Context, synth
     S, _ = CONFIG_SHAPES[args.workload]
+    KL = int(getattr(args, "key_len", 16))
     dev = torch.device("cuda", 0)
     ctx = Context(0, S)
-    keys = synth.keys(0, S).reshape(-1)
+    # 16-byte keys: the synthetic sessions' own keys; other lengths: seeded
+    # random bytes (the key schedule's register / window / fetch paths,
+    # DESIGN.md §3.7)
+    keys = synth.keys(0, S).reshape(-1) if KL == 16 else \
+        np.random.default_rng(5).integers(0, 256, S * KL, dtype=np.uint8)
     T = lambda a: torch.from_numpy(a).to(dev)
-    kl = T(np.full(S, 16, dtype=np.int32))
-    ko = T(np.arange(S, dtype=np.int64) * 16)
+    kl = T(np.full(S, KL, dtype=np.int32))
+    ko = T(np.arange(S, dtype=np.int64) * KL)
     kd = T(keys)
     st = torch.cuda.current_stream(dev)
     for _ in range(args.warmup):
@@ -599,18 +604,18 @@ def ksa_storm(args):
     per = statistics.median(a.elapsed_time(b) / m for a, b, m in seg) * 1e-3   # s per launch
     out = {"metric": "RC4 KSA streams/s (batched makeSBox, connection storm)",
            "value": round(S / per, 1), "unit": "streams/s", "workload": args.workload,
-           "streams_per_launch": S, "key_bytes": 16, "kernel_us": round(per * 1e6, 3),
+           "streams_per_launch": S, "key_bytes": KL, "kernel_us": round(per * 1e6, 3),
            "ns_per_stream": round(per * 1e9 / S, 4), "wall_streams_per_s": round(S * args.steps / wall, 1),
-           "algorithmic_bytes_per_launch": S * (16 + 8 + 4 + STATE_BYTES // 2),
+           "algorithmic_bytes_per_launch": S * (KL + 8 + 4 + STATE_BYTES // 2),
            "note": "key + offset/len read, 258-B state written per stream; not the headline value"}
     if args.cpu_seconds > 0:
         sys.path.insert(0, str(ROOT / "oracle"))
         import pyoracle  # cpu_baseline leg only
         n = min(S, 65536)
         ob = pyoracle.Batch(n)
-        kh = keys[: 16 * n]
-        offs = np.arange(n, dtype=np.uint64) * 16
-        lens = np.full(n, 16, dtype=np.uint32)
+        kh = keys[: KL * n]
+        offs = np.arange(n, dtype=np.uint64) * KL
+        lens = np.full(n, KL, dtype=np.uint32)
         runs, t_end = [], time.perf_counter() + args.cpu_seconds
         while len(runs) < 5 or time.perf_counter() < t_end:
             t1 = time.perf_counter()
@@ -620,7 +625,7 @@ def ksa_storm(args):
                 break
         cpu = statistics.median(runs)
         out["cpu_baseline"] = {"value": round(cpu, 1), "unit": "streams/s", "cores": 1, "kind": "port",
-                               "sample": f"{n} x 16-byte keys, oracle make_sbox batch, median of {len(runs)} runs"}
+                               "sample": f"{n} x {KL}-byte keys, oracle make_sbox batch, median of {len(runs)} runs"}
         out["speedup_vs_1_core"] = round(S / per / cpu, 1)
     return out
 
@@ -761,6 +766,7 @@ def parse(argv=None):
                    help="launches per HIP-event segment (kernel duration = segment time / N)")
     p.add_argument("--host-inclusive", action="store_true",
                    help="measure the PCIe-inclusive rate instead (DESIGN.md), one JSON line")
+    p.add_argument("--key-len", type=int, default=16, help="with --ksa: key bytes per session")
     p.add_argument("--ksa", action="store_true",
                    help="measure the connection-storm KSA rate instead (DESIGN.md), one JSON line")
     p.add_argument("--frame", action="store_true",
@@ -773,8 +779,8 @@ def parse(argv=None):
     p.add_argument("--companion-steps", type=int, default=100)
     p.add_argument("--companion-warmup", type=int, default=120)
     p.add_argument("--chunks", type=int, default=0,
-                   help="with --host-inclusive: chunks of the batch (0 = by size: one up to 8 MiB, else one per "
-                        "2 MiB up to 16; tools/hostinc_sweep.py)")
+                   help="with --host-inclusive: chunks of the batch (0 = by size, host_chunks: one up to 32 MiB, "
+                        "else one per 32 MiB, at most 16; tools/hostinc_sweep.py)")
     p.add_argument("--streams", type=int, default=4)
     return p.parse_args(argv)
 

@@ -60,10 +60,11 @@ extern "C" {
 #define ZRC4_ERR_LAUNCH (-4)
 #define ZRC4_ERR_SLOT_RANGE (-5)
 #define ZRC4_ERR_HIP (-6)
-#define ZRC4_ERR_GROUP (-7)    /* zrc4_crypt_grouped: a bucket mixes slot groups */
+#define ZRC4_ERR_GROUP (-7)    /* zrc4_crypt_grouped: a bucket broke the bucket contract */
 #define ZRC4_ERR_INTERNAL (-8) /* kernel self-check failed (LDS layout) */
-#define ZRC4_ERR_STATE (-9)    /* zrc4_ks: the slot's stream position was lost by a failed
-                                  crypt; reseed (zrc4_ks_make_sbox) or copy into it */
+#define ZRC4_ERR_STATE (-9)    /* zrc4_ks_crypt / zrc4_ks_copy: the slot's stream position
+                                  was lost by a failed zrc4_ks_crypt; reseed it
+                                  (zrc4_ks_make_sbox) or copy into it (zrc4_ks_copy) */
 
 /* Slots are grouped 256 to a 64 KiB device image (the LDS image of one
  * workgroup); capacity is rounded up to a multiple of this. */
@@ -112,9 +113,21 @@ int zrc4_crypt_range(zrc4_ctx *ctx, uint32_t first_slot, uint8_t *payload,
  * that group, and that a slot appears at most once.  Entries may come in any
  * order; padding entries carry ids[i] = ZRC4_IDLE_SLOT or len 0.  Each bucket
  * then moves its group's state as one coalesced 64 KiB image, exactly like a
- * whole-group zrc4_crypt_range.  A bucket whose busy entries span two groups
- * is skipped and reported by zrc4_sync as ZRC4_ERR_GROUP.  Device pointers;
- * asynchronous. */
+ * whole-group zrc4_crypt_range.  Refusals, reported by zrc4_sync as
+ * ZRC4_ERR_GROUP (no payload byte, S-box or x/y of a refused bucket is
+ * touched; every other bucket runs):
+ *   - a bucket whose busy entries span two groups, or name a slot twice;
+ *   - a bucket naming a group another bucket of the same call holds: every
+ *     bucket claims (the part of) its group it moves, and the first claimant
+ *     runs.  With more buckets than CUs each bucket is checked before it
+ *     claims; with fewer, the claim is taken on the bucket's first busy id
+ *     while the check runs, so a bucket that breaks the one-group rule may
+ *     also block the valid bucket of the group its first id names.
+ * An id >= capacity other than ZRC4_IDLE_SLOT is skipped and reported as
+ * ZRC4_ERR_SLOT_RANGE (the rest of its bucket runs).  The claims carry a
+ * per-call tag chosen on the host: a grouped call must not be captured into
+ * a HIP graph and replayed (the replay would find its own tags and refuse
+ * every bucket).  n <= 0xFFF00000.  Device pointers; asynchronous. */
 #define ZRC4_IDLE_SLOT 0xFFFFFFFFu
 int zrc4_crypt_grouped(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payload,
                        const uint64_t *off, const uint32_t *len, uint32_t n,
@@ -122,7 +135,9 @@ int zrc4_crypt_grouped(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payload,
 
 /* Host-pointer variants: copy to the device (pinned staging), run, copy back,
  * block until done.  payload_bytes bounds the host payload buffer.
- * zrc4_crypt_host with several ids buckets them by group itself and runs the
+ * zrc4_crypt_host checks every id on the host first: an id >= capacity
+ * (ZRC4_IDLE_SLOT included) returns ZRC4_ERR_SLOT_RANGE and crypts nothing.
+ * With several ids it buckets them by group itself and runs the
  * zrc4_crypt_grouped path (a slot may appear once per call: a repeated slot
  * returns ZRC4_ERR_INVALID_ARG and crypts nothing). */
 int zrc4_ksa_host(zrc4_ctx *ctx, const uint32_t *ids, const uint8_t *keys,
@@ -213,7 +228,13 @@ int zrc4_crypt_grouped_frame(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payloa
  * value (device state + buffered keystream).  ring_bytes 0: no buffering
  * (every call crypts on the device).  Thread-safe per reservoir; a slot at
  * most once per zrc4_ks_crypt call.  stats: ring bytes, tail bytes, tail
- * launches, refill bytes, refill launches, refill waits. */
+ * launches, refill bytes, refill launches, refill waits.
+ * Failure: a zrc4_ks_crypt whose device tail fails returns the error and
+ * leaves EVERY slot of that call lost (some spans may already be crypted
+ * from their rings, some not): zrc4_ks_crypt and zrc4_ks_copy return
+ * ZRC4_ERR_STATE for them until zrc4_ks_make_sbox reseeds a slot or
+ * zrc4_ks_copy copies a live one into it; the call's data must be treated as
+ * consumed, not retried. */
 typedef struct zrc4_ks zrc4_ks;
 int zrc4_ks_create(zrc4_ctx *ctx, uint32_t ring_bytes, zrc4_ks **out);
 int zrc4_ks_destroy(zrc4_ks *ks);

@@ -935,13 +935,14 @@ def test_window_tag_restart(built, torch_cuda):
 def test_reservoir_failed_tail_loses_position_until_reseeded(built, monkeypatch):
     """a reservoir tail crypt that fails must not let the slot go
     on from an unknown keystream position.  With the test hook
-    ZRC4_KS_FAIL_TAIL_AFTER=2 the second tail crypt of the reservoir fails:
+    ZRC4_KS_FAIL_TAIL_AFTER=2 (read only by the ZRC4_TEST_HOOKS build,
+    libzrc4_testhooks.so) the second tail crypt of the reservoir fails:
     that call returns the error, every later call on the slot returns
     ZRC4_ERR_STATE (-9) and touches nothing, another slot is unaffected, and
     zrc4_ks_make_sbox reseeds it back to reference bytes."""
     import ctypes as C
-    from zsummerx_amd import _capi
-    lib = _capi.load()
+    from zsummerx_amd import _capi, build
+    lib = _capi.load(build.PKG / "libzrc4_testhooks.so")
     monkeypatch.setenv("ZRC4_KS_FAIL_TAIL_AFTER", "2")
     ctx, ks = C.c_void_p(), C.c_void_p()
     assert lib.zrc4_create(C.byref(ctx), 0, 256) == 0

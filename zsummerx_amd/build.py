@@ -211,7 +211,8 @@ def build_oracle() -> None:
 
 # A/B builds the GPU tests load (tests/test_gpu_parity.py): built with the
 # product so that no test compiles on the GPU box.
-TEST_VARIANTS = {"wintag4": {"ZRC4_WIN_TAG_LIMIT": 4}}
+TEST_VARIANTS = {"wintag4": {"ZRC4_WIN_TAG_LIMIT": 4},
+                 "testhooks": {"ZRC4_TEST_HOOKS": 1}}      # fault injection (zrc4_ks.inc), never the product
 
 
 def build_all(force: bool = False) -> None:

@@ -8,6 +8,7 @@
 #include "zrc4_win.hpp"
 
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>

@@ -631,13 +631,17 @@ __device__ __forceinline__ void preload_line0(u32x32 &P, const LineSetup &ls, co
     preload_line(P, nb > 0 ? p : sk, nb > 1 ? p + 64 : sk + 64);
 }
 
-// Line 0 of the next group from asm (ZRC4_LINE0_ASM): issued after the
-// keystream, before the image copy-out, and waited for after the next fill
-// with a counted vmcnt(16) (the 16 image stores are the only younger VMEM
-// ops) -- as compiler loads, the compiler drains everything there
-// (vmcnt(0)), the image stores included.
+// Line 0 of the next group from asm (ZRC4_LINE0_ASM, r04 A/B knob, off):
+// issued after the keystream, before the image copy-out, and waited for
+// after the next fill with a counted vmcnt(16) (the 16 image stores are the
+// only younger VMEM ops); as compiler loads the compiler drains everything
+// there (vmcnt(0)), the image stores included.  Same-process medians
+// (profiles/r04/grp/ab_range.log, ab_grouped.log): cfg5 287.2 vs 286.2 us,
+// grouped cfg5 298.0 vs 296.4 -- the drain costs nothing measurable (most
+// 1 KiB groups load line 0 inside the last half, p_async), so the simpler
+// compiler form stays.
 #ifndef ZRC4_LINE0_ASM
-#define ZRC4_LINE0_ASM 1
+#define ZRC4_LINE0_ASM 0
 #endif
 __device__ __forceinline__ void issue_line0_asm(u32x32 &P, const LineSetup &ls, const uint8_t *sk)
 {
@@ -2026,6 +2030,31 @@ __device__ __forceinline__ void ksa64_pattern_asm(uint32_t &x0, uint32_t &x1, ui
         : "memory");
 }
 
+// 16 KSA steps with the key bytes of a 17-byte window in registers (q[0..3]
+// and byte 0 of q[4]): step u adds window byte u + 1 (the off-pattern key
+// lengths, ksa_kernel's window path).
+__device__ __forceinline__ void ksa16_window_asm(uint32_t &x0, uint32_t &x1, uint32_t &a0, uint32_t &ya,
+                                                 const uint32_t (&q)[5])
+{
+    uint32_t a1, b;
+    asm volatile(
+        ZRC4_KSA_QPAIR(q0, BYTE_1, q0, BYTE_2) ZRC4_KSA_QPAIR(q0, BYTE_3, q1, BYTE_0)
+        ZRC4_KSA_QPAIR(q1, BYTE_1, q1, BYTE_2) ZRC4_KSA_QPAIR(q1, BYTE_3, q2, BYTE_0)
+        ZRC4_KSA_QPAIR(q2, BYTE_1, q2, BYTE_2) ZRC4_KSA_QPAIR(q2, BYTE_3, q3, BYTE_0)
+        ZRC4_KSA_QPAIR(q3, BYTE_1, q3, BYTE_2) ZRC4_KSA_QPAIR(q3, BYTE_3, q4, BYTE_0)
+        "s_waitcnt lgkmcnt(0)\n\t"
+        : [ya] "+v"(ya), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0), [a1] "=&v"(a1), [b] "=&v"(b)
+        : [q0] "v"(q[0]), [q1] "v"(q[1]), [q2] "v"(q[2]), [q3] "v"(q[3]), [q4] "v"(q[4])
+        : "memory");
+}
+
+// ksa_kernel's LDS: the 64 KiB S-box image, then 16 KiB of key schedule
+// prefixes (window path: dword w of lane j at kKsaSched + 4 * (w * 256 + j),
+// conflict-free for any per-lane w).  80 KiB: two workgroups per CU.
+constexpr uint32_t kKsaSched = kGroupBytes;
+constexpr uint32_t kKsaWinMax = 48;            // window path: key lengths up to this (16c mod len + 17 <= 64)
+constexpr uint32_t kSmemKsa = kGroupBytes + 16384;
+
 __global__ void __launch_bounds__(256, 2)
 ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
            const uint32_t *__restrict__ ids, uint32_t first_slot,
@@ -2033,7 +2062,7 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
            const uint64_t *__restrict__ key_off, const uint32_t *__restrict__ key_len,
            uint32_t n, uint32_t capacity, uint32_t *__restrict__ err)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kGroupBytes + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kSmemKsa];
     uint8_t *S = smem;
     if (!lds_base_ok(S, err)) return;
 
@@ -2069,6 +2098,41 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     }
     const bool partial = (blockIdx.x + 1u) * kGroup > n;
     const uint32_t col = col_of(j);
+
+    // Window path (key lengths that do not divide 16 and are not 32 / 64,
+    // up to kKsaWinMax): the first 64 bytes of this lane's key schedule,
+    // E[i] = key[i mod len] (rc4_encryption.h:67-70), go to LDS once, before
+    // the S-boxes are filled.  The key arrives as the <= 13 dwords that cover
+    // it (not 64 per-lane byte loads: each byte-load instruction of a wave
+    // touches ~20 cache lines), parked in the S-box area (free until the
+    // fill), and E is assembled from LDS bytes.  Layouts are transposed
+    // (dword w of lane j at 4 * (w * 256 + j)): conflict-free.
+    const bool winpath = active && kl != 0u && kl <= kKsaWinMax && !(kl <= 16u && (16u % kl) == 0u) &&
+                         kl != 32u && kl != 64u;
+    uint32_t *sch = reinterpret_cast<uint32_t *>(smem + kKsaSched) + j;
+    if (winpath) {
+        const uintptr_t ka = (uintptr_t)key;
+        const uint32_t *kw = reinterpret_cast<const uint32_t *>(ka & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(ka & 3u), nw = (sh + kl + 3u) >> 2;   // dwords overlapping the key
+        uint32_t *raw = reinterpret_cast<uint32_t *>(smem) + j;
+#pragma unroll
+        for (uint32_t w = 0; w < 13u; ++w)
+            if (w < nw) raw[w * 256u] = kw[w];
+        const uint8_t *rb = smem + 4u * j;
+        uint32_t m = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t p_ = sh + m;
+                v |= (uint32_t)rb[(p_ >> 2) * 1024u + (p_ & 3u)] << (8 * b);
+                if (++m == kl) m = 0;
+            }
+            sch[w * 256] = v;
+        }
+    }
+    __syncthreads();                                 // the S-box area is free again
 
     // Identity boxes (:50-53): a whole, fully re-seeded group fills its 64 KiB
     // image cooperatively (row k = 256 copies of k, 16 x 16 B per lane);
@@ -2110,6 +2174,34 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col];
             uint32_t ya = col | ((q[0] & 0xFFu) << 8);
             for (int c = 0; c < 4; ++c) ksa64_pattern_asm(x0, x1, a0, ya, q);
+        } else if (winpath) {
+            // The 17 bytes chunk c needs are E[k .. k+16] with k = 16c mod len
+            // (<= 47): 5 dwords + byte aligns, read one chunk ahead (the reads
+            // retire ahead of the first step's own LDS round trip).  The
+            // per-chunk global byte loads of the fetch path below cost 1.4-2x
+            // at 24-40-byte keys.
+            uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col];
+            uint32_t ya = col | ((sch[0] & 0xFFu) << 8);   // j = 0 + key[0] before step 0
+            uint32_t k = 0;                                // 16c mod len
+            uint32_t d[5];
+#pragma unroll
+            for (int m = 0; m < 5; ++m) d[m] = sch[m * 256];
+            for (int c = 0; c < 16; ++c) {
+                const uint32_t sh = 8u * (k & 3u);
+                uint32_t q[5];
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    q[m] = (uint32_t)(((uint64_t)d[m + 1] << 32 | d[m]) >> sh);
+                q[4] = d[4] >> sh;
+                k += 16u;
+                while (k >= kl) k -= kl;
+                if (c < 15) {
+                    const uint32_t i0 = k >> 2;
+#pragma unroll
+                    for (int m = 0; m < 5; ++m) d[m] = sch[(i0 + m) * 256];
+                }
+                ksa16_window_asm(x0, x1, a0, ya, q);
+            }
         } else {
             // key bytes of steps 16c .. 16c+16, fetched one chunk ahead
             uint32_t kk = 0;
