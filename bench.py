@@ -662,7 +662,7 @@ def frame_bench(args):
     import torch
     from zsummerx_amd import Context
     S, L = CONFIG_SHAPES[args.workload]
-    S = min(S, 131072)
+    S = min(S, 524288)
     dev = torch.device("cuda", 0)
     buf, npk_total = frame_payload(S, L)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
@@ -694,29 +694,48 @@ def frame_bench(args):
         ctx.sync(st)
         got_npk = int(npk.sum().item())
         scratch = T(np.zeros(S * L, dtype=np.uint8))
-        t_crypt = timed(lambda: ctx.crypt_range(0, scratch, d_off, d_len, n=S, stream=st))
-        ctx.sync(st)
         # Decrypt + frame: each session's block = [L bytes of packets | L-byte
         # fresh tail]; the tail is decrypted, the packet part framed (kept out
         # of the decrypt so repeated launches frame the same packets).  Fused
-        # (zrc4_crypt_range_frame: one launch) vs two launches.
+        # (zrc4_crypt_range_frame / zrc4_crypt_grouped_frame: one launch) vs
+        # two launches (the crypt, then zrc4_frame_scan).  --ids grouped:
+        # entries bucketed by group, slots permuted inside each group and the
+        # groups in random order (the session engine's shape).
         blk = np.zeros(S * 2 * L, dtype=np.uint8)
         blk.reshape(S, 2 * L)[:, :L] = buf.reshape(S, L)
         d_blk = T(blk)
-        f_off = T((np.arange(S, dtype=np.int64) * 2 * L))
-        t_off = T((np.arange(S, dtype=np.int64) * 2 * L + L))
+        perm = np.arange(S, dtype=np.int64)
+        if args.ids == "grouped":
+            rng = np.random.default_rng(77)
+            pos = 0
+            for g in rng.permutation(-(-S // 256)):
+                lo, hi = g * 256, min((g + 1) * 256, S)
+                perm[pos:pos + hi - lo] = lo + rng.permutation(hi - lo)
+                pos += hi - lo
+        d_ids = T(perm.astype(np.int32))
+        f_off = T(perm * 2 * L)
+        t_off = T(perm * 2 * L + L)
+        if args.ids == "grouped":
+            crypt = lambda p, o: ctx.crypt_grouped(p, o, d_len, d_ids, n=S, stream=st)
+            fused = lambda fr: ctx.crypt_grouped_frame(d_blk, t_off, d_len, d_ids, fr, n=S, stream=st)
+        else:
+            crypt = lambda p, o: ctx.crypt_range(0, p, o, d_len, n=S, stream=st)
+            fused = lambda fr: ctx.crypt_range_frame(0, d_blk, t_off, d_len, fr, n=S, stream=st)
+        d_off_e = T(perm * L)                            # entry e -> session perm[e]'s L bytes of scratch
+        t_crypt = timed(lambda: crypt(scratch, d_off_e))
+        ctx.sync(st)
         frame = {"off": f_off, "len": d_len, "bound": bound, "npk": npk, "used": used, "status": status}
-        t_fused = timed(lambda: ctx.crypt_range_frame(0, d_blk, t_off, d_len, frame, n=S, stream=st))
+        t_fused = timed(lambda: fused(frame))
         ctx.sync(st)
         fused_npk = int(npk.sum().item())
 
         def two_launches():
-            ctx.crypt_range(0, d_blk, t_off, d_len, n=S, stream=st)
+            crypt(d_blk, t_off)
             ctx.frame_scan(d_blk, f_off, d_len, bound, npk, used, status, stream=st)
         t_two = timed(two_launches)
         ctx.sync(st)
     out = {"metric": "proto4z frame scan (device-resident, decrypted buffers)", "workload": args.workload,
-           "sessions": S, "bytes_per_session": L, "packets_per_launch": got_npk,
+           "ids": args.ids, "sessions": S, "bytes_per_session": L, "packets_per_launch": got_npk,
            "packets_expected": npk_total, "kernel_us": round(t_scan * 1e6, 3),
            "framed_gib_s": round(S * L / t_scan / GIB, 2), "packets_per_s": round(got_npk / t_scan, 1),
            "crypt_kernel_us_same_batch": round(t_crypt * 1e6, 3),

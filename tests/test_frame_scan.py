@@ -182,11 +182,14 @@ def _fused_case(n, avg, seed, tail_frac=0.5):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,avg,mode", [(4096, 900, "range"), (1000, 3000, "grouped"), (70000, 200, "range")])
+@pytest.mark.parametrize("n,avg,mode", [(4096, 900, "range"), (1000, 3000, "grouped"), (70000, 200, "range"),
+                                        (150000, 200, "grouped"), (600000, 40, "range"), (600000, 40, "grouped")])
 def test_fused_decrypt_and_frame(built, n, avg, mode):
     """zrc4_crypt_*_frame: decrypt the fresh tail and frame the WHOLE block in
-    one launch (fused epilogue at <= 1 group per CU; the 70 000-session case
-    exceeds one group per CU and takes the throughput kernel + scan launch).
+    one launch: the direct kernels' epilogue at <= 1 group per CU, the
+    persistent kernel's tail above (70 000 / 150 000 sessions: 274 / 587
+    groups, one or two chunks per workgroup; 600 000: 2 344 groups, five
+    chunks per workgroup, the tail's four-walk lockstep plus a remainder).
     Plaintext and framing against the oracle."""
     import torch
     from zsummerx_amd import Context

@@ -70,15 +70,16 @@ def test_edge_cases(ctx, edge):
 
 
 def test_ksa_key_lengths_batched(built, torch_cuda):
-    """Batched makeSBox over key lengths 0..40, 63, 64, 65, 128, 255, 256,
+    """Batched makeSBox over key lengths 0..50, 63, 64, 65, 128, 255, 256,
     257, 300: the 16-byte register pattern takes lengths 1, 2, 4, 8, 16, the
-    64-byte register pattern 32 and 64, every other length (65 and 128 pin
-    the edges of the 64-byte branch) fetches key bytes per step; NUL bytes
-    included, keys at odd offsets; whole groups (range) and scattered ids;
-    states against the oracle."""
+    64-byte register pattern 32 and 64, the LDS window path every other
+    length up to 48 (49 and 50 pin its edge), the rest fetch key bytes per
+    step (65 and 128 pin the edges of the 64-byte branch); NUL bytes
+    included, keys at every alignment; whole groups (range) and scattered
+    ids; states against the oracle."""
     torch = torch_cuda
     rng = np.random.default_rng(31)
-    lens = list(range(0, 41)) + [63, 64, 65, 128, 255, 256, 257, 300]
+    lens = list(range(0, 51)) + [63, 64, 65, 128, 255, 256, 257, 300]
     n = 512
     klen = np.array([lens[i % len(lens)] for i in range(n)], dtype=np.uint32)
     koff = (np.concatenate([[3], np.cumsum(klen[:-1] + 1) + 3])).astype(np.uint64)

@@ -92,7 +92,7 @@ def disassemble(lib: Path) -> str:
 
 
 def kernel_resources(lib: Path) -> dict:
-    """Per kernel: VGPRs, VGPR / SGPR spills and LDS bytes, from the code
+    """Per kernel: VGPRs, VGPR / SGPR spills, scratch and LDS bytes, from the code
     object's AMDGPU metadata note."""
     with tempfile.TemporaryDirectory() as td:
         co = _unbundle(lib, td)
@@ -101,7 +101,7 @@ def kernel_resources(lib: Path) -> dict:
     out, cur = {}, {}
     for line in notes.splitlines():
         m = re.match(r"\s*(?:- )?\.(agpr_count|name|vgpr_count|vgpr_spill_count|sgpr_spill_count|"
-                     r"group_segment_fixed_size):\s+(\S+)", line)
+                     r"group_segment_fixed_size|private_segment_fixed_size):\s+(\S+)", line)
         if not m:
             continue
         k, v = m.groups()

@@ -88,8 +88,8 @@ constexpr size_t kZeroCopyMax = 256u << 10;   // *_host batches up to this size 
 // transpose); otherwise one group per workgroup (crypt_kernel: chain-bound,
 // per-lane stores).  A/B: the DPP path is 5-7 us slower at one group per CU
 // (cfg2 56.1 vs 48.8 us, cfg3 28.1 vs 22.7 us; profiles/r02_ab_dpp_direct.log).
-// With `fr`, the framing walk of every entry runs too: fused into the direct
-// kernel's epilogue, or -- behind the throughput kernel -- as a second launch.
+// With `fr`, the framing walk of every entry runs in the same launch: in the
+// direct kernels' epilogue, or in the persistent kernel's tail.
 int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot, uint8_t *payload,
                  const uint64_t *off, const uint32_t *len, uint32_t n, hipStream_t s,
                  const zrc4::FrameArgs *fr = nullptr)
@@ -170,24 +170,29 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
             return ZRC4_ERR_INVALID_ARG;
         return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
     }
-    if (fr) {
-        const int rc = launch_crypt(c, mode, ids, first_slot, payload, off, len, n, s, nullptr);
-        if (rc != ZRC4_OK) return rc;
-        hipLaunchKernelGGL(zrc4::frame_scan_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, payload, fr->off,
-                           fr->len, fr->bound, n, fr->maxp, fr->npk, fr->used, fr->status, fr->pkt_len);
-        return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
-    }
     if (stream_kernel) {
+        // with `fr`, the framing walk runs in the same launch, in each
+        // workgroup's tail over the chunks it decrypted (frame_walk_chunks)
         const uint32_t wgs = std::min(grid, 2u * (uint32_t)c->num_cus);
+        const zrc4::FrameArgs fa = fr ? *fr : zrc4::FrameArgs{};
+#define ZRC4_STREAM(PF_, GR_)                                                                                   \
+    do {                                                                                                       \
+        if (fr)                                                                                                \
+            hipLaunchKernelGGL((zrc4::crypt_stream_kernel<PF_, GR_, true>), dim3(wgs), blk, 0, s, c->arena,    \
+                               c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, cl, \
+                               fa);                                                                            \
+        else                                                                                                   \
+            hipLaunchKernelGGL((zrc4::crypt_stream_kernel<PF_, GR_, false>), dim3(wgs), blk, 0, s, c->arena,   \
+                               c->xy, ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, cl, \
+                               fa);                                                                            \
+    } while (0)
         if (mode == zrc4::kGrouped)
-            hipLaunchKernelGGL((zrc4::crypt_stream_kernel<true, true>), dim3(wgs), blk, 0, s, c->arena, c->xy, ids,
-                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink, cl);
+            ZRC4_STREAM(true, true);
         else if (mode == zrc4::kRange && (first_slot & 255u) == 0u)
-            hipLaunchKernelGGL((zrc4::crypt_stream_kernel<true, false>), dim3(wgs), blk, 0, s, c->arena, c->xy, ids,
-                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink, cl);
+            ZRC4_STREAM(true, false);
         else
-            hipLaunchKernelGGL((zrc4::crypt_stream_kernel<false, false>), dim3(wgs), blk, 0, s, c->arena, c->xy,
-                               ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, cl);
+            ZRC4_STREAM(false, false);
+#undef ZRC4_STREAM
     } else if (mode == zrc4::kRange) {
         hipLaunchKernelGGL(zrc4::crypt_kernel<zrc4::kRange>, dim3(grid), blk, 0, s, c->arena, c->xy, ids,
                            first_slot, payload, off, len, n, c->capacity, c->err, c->sink);

@@ -102,6 +102,17 @@ __device__ __forceinline__ uint32_t col_of(uint32_t j)
     return ((l & 31u) << 2) | (l >> 5) | ((w & 1u) << 1) | ((w >> 1) << 7);
 }
 
+// The persistent kernel's image moves (prefetch, LDS fill, copy-out): thread
+// j takes the 16-byte chunks at img_vo(j) + 4096 i, i < 16.  Waves 2p and
+// 2p+1 (the two waves whose columns have bit 7 = p, col_of) move exactly
+// bytes [128p, 128p + 128) of every 256-byte row -- their own half of the
+// image, one whole 128-byte line per 8 lanes -- so a wave pair can fill and
+// copy out its half without the other pair.
+__device__ __forceinline__ uint32_t img_vo(uint32_t j)
+{
+    return (((j & 127u) >> 3) << 8) | (j & 128u) | ((j & 7u) << 4);
+}
+
 // ---------------------------------------------------------------------------
 // Diagnostic timing build (ZRC4_TIMING=1, never the product): lane 0 of each
 // wave stamps s_memrealtime (100 MHz) and s_memtime (shader clock) at kernel
@@ -954,20 +965,37 @@ __device__ __forceinline__ uint32_t load_le32(const uint8_t *p)
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// HasRawPacket's checks (proto4z.h:704-748) around one header read at u:
+// frame_pre before it (0 = read the header), frame_post after it (0 = a
+// complete packet of pl bytes); otherwise the stop status.
+__device__ __forceinline__ uint32_t frame_pre(uint32_t L, uint32_t u, uint32_t bound)
+{
+    const uint32_t cur = L - u, bl = bound - u;
+    if (bl < cur || bound < bl) return 2u;                        // :708-711
+    if (cur < 6u) return 1u;                                      // :715-718 (headLen = 4 + 2, :714)
+    return 0u;
+}
+
+__device__ __forceinline__ uint32_t frame_post(uint32_t pl, uint32_t L, uint32_t u, uint32_t bound)
+{
+    const uint32_t cur = L - u, bl = bound - u;
+    if (pl < 6u) return 2u;                                       // :718-721
+    if (pl > bl) return pl > bound ? 2u : 1u;                     // :722-732
+    if (pl > bound) return 2u;                                    // :735-738
+    if (pl > cur) return 1u;                                      // :747
+    return 0u;
+}
+
 __device__ __forceinline__ void frame_walk(const uint8_t *b, uint32_t L, uint32_t bound, uint32_t maxp, uint32_t e,
                                            uint32_t *npk, uint32_t *used, uint32_t *status, uint32_t *pkt_len)
 {
-    const uint32_t headLen = 4u + 2u;          // sizeof(LenInteger) + sizeof(ProtoInteger), proto4z.h:714
     uint32_t u = 0, k = 0, st;
     for (;;) {
-        const uint32_t cur = L - u, bl = bound - u;
-        if (bl < cur || bound < bl) { st = 2u; break; }              // :708-711
-        if (cur < headLen) { st = 1u; break; }                       // :715-718
-        const uint32_t pl = load_le32(b + u);                        // ReadPodData, :717
-        if (pl < headLen) { st = 2u; break; }                        // :718-721
-        if (pl > bl) { st = pl > bound ? 2u : 1u; break; }          // :722-732
-        if (pl > bound) { st = 2u; break; }                          // :735-738
-        if (pl > cur) { st = 1u; break; }                            // :747
+        st = frame_pre(L, u, bound);
+        if (st) break;
+        const uint32_t pl = load_le32(b + u);                     // ReadPodData, :717
+        st = frame_post(pl, L, u, bound);
+        if (st) break;
         if (pkt_len && k < maxp) pkt_len[(size_t)e * maxp + k] = pl;
         ++k;
         u += pl;
@@ -975,6 +1003,63 @@ __device__ __forceinline__ void frame_walk(const uint8_t *b, uint32_t L, uint32_
     npk[e] = k;
     used[e] = u;
     status[e] = st;
+}
+
+// The framing of every entry of the 256-entry chunks c0, c0 + step, ... <
+// nchunks (entry c * 256 + lane): the persistent kernel's tail, after its own
+// stores have landed.  Four chunks' walks advance in lockstep, so a lane's
+// four header reads per round are in flight together (each walk is a chain
+// of dependent round trips).
+__device__ __forceinline__ void frame_walk_chunks(const uint8_t *payload, const FrameArgs &fr, uint32_t c0,
+                                                  uint32_t step, uint32_t nchunks, uint32_t n, uint32_t lane)
+{
+    constexpr int kW = 4;
+    for (uint32_t c = c0; c < nchunks; c += kW * step) {
+        const uint8_t *b[kW];
+        uint32_t L[kW], u[kW], k[kW], st[kW], e[kW];
+        bool live[kW], valid[kW];
+#pragma unroll
+        for (int i = 0; i < kW; ++i) {
+            const uint32_t ci = c + (uint32_t)i * step;
+            e[i] = ci * kGroup + lane;
+            valid[i] = ci < nchunks && e[i] < n;
+            live[i] = valid[i];
+            b[i] = payload + (valid[i] ? fr.off[e[i]] : 0u);
+            L[i] = valid[i] ? fr.len[e[i]] : 0u;
+            u[i] = k[i] = st[i] = 0u;
+        }
+        while (live[0] || live[1] || live[2] || live[3]) {
+            uint32_t pl[kW];
+#pragma unroll
+            for (int i = 0; i < kW; ++i) {
+                if (live[i]) {
+                    st[i] = frame_pre(L[i], u[i], fr.bound);
+                    live[i] = st[i] == 0u;
+                    if (live[i]) pl[i] = load_le32(b[i] + u[i]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kW; ++i) {
+                if (live[i]) {
+                    st[i] = frame_post(pl[i], L[i], u[i], fr.bound);
+                    live[i] = st[i] == 0u;
+                    if (live[i]) {
+                        if (fr.pkt_len && k[i] < fr.maxp) fr.pkt_len[(size_t)e[i] * fr.maxp + k[i]] = pl[i];
+                        ++k[i];
+                        u[i] += pl[i];
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kW; ++i) {
+            if (valid[i]) {
+                fr.npk[e[i]] = k[i];
+                fr.used[e[i]] = u[i];
+                fr.status[e[i]] = st[i];
+            }
+        }
+    }
 }
 
 // LDS of crypt_kernel: the 64 KiB S-box image at offset 0 (the asm's absolute
@@ -1390,12 +1475,11 @@ __device__ __forceinline__ void prefetch_group(u32x32 &P, u32x32 &Q, u32x32 &ilo
                                                const uint32_t *alen, const uint64_t *aoff,
                                                const uint16_t *axy, const uint8_t *ibase, uint32_t j)
 {
-    uint32_t vo;
+    uint32_t vo = img_vo(j);
     asm volatile(
         "global_load_dword %[rlen], %[alen], off\n\t"
         "global_load_dwordx2 %[roff], %[aoff], off\n\t"
         "global_load_ushort %[rxy], %[axy], off\n\t"
-        "v_lshlrev_b32 %[vo], 4, %[j]\n\t"
         "global_load_dwordx4 v[160:163], %[vo], %[ib]\n\t"
         "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
         "global_load_dwordx4 v[164:167], %[vo], %[ib]\n\t"
@@ -1428,8 +1512,8 @@ __device__ __forceinline__ void prefetch_group(u32x32 &P, u32x32 &Q, u32x32 &ilo
         "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
         "global_load_dwordx4 v[220:223], %[vo], %[ib]\n\t"
         : "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[160:191]}"(ilo), "=&{v[192:223]}"(ihi),
-          [rlen] "=&v"(rlen), [roff] "=&v"(roff), [rxy] "=&v"(rxy), [vo] "=&v"(vo)
-        : [alen] "v"(alen), [aoff] "v"(aoff), [axy] "v"(axy), [ib] "s"(ibase), [j] "v"(j)
+          [rlen] "=&v"(rlen), [roff] "=&v"(roff), [rxy] "=&v"(rxy), [vo] "+v"(vo)
+        : [alen] "v"(alen), [aoff] "v"(aoff), [axy] "v"(axy), [ib] "s"(ibase)
         : "memory");
 }
 
@@ -1539,7 +1623,7 @@ __device__ __forceinline__ void prefetch_bucket(u32x32 &P, u32x32 &Q, u32x32 &il
                                                 const uint16_t *axy, const uint32_t *aqid, const uint32_t *aqlen,
                                                 const uint8_t *ibase, uint32_t j)
 {
-    uint32_t vo;
+    uint32_t vo = img_vo(j);
     uint64_t sv;
     asm volatile(
         "s_mov_b64 %[sv], exec\n\t"
@@ -1557,7 +1641,6 @@ __device__ __forceinline__ void prefetch_bucket(u32x32 &P, u32x32 &Q, u32x32 &il
         "global_load_ushort %[rxy], %[axy], off\n\t"
         "global_load_dword %[qid], %[aqid], off\n\t"
         "global_load_dword %[qlen], %[aqlen], off\n\t"
-        "v_lshlrev_b32 %[vo], 4, %[j]\n\t"
         "global_load_dwordx4 v[160:163], %[vo], %[ib]\n\t"
         "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
         "global_load_dwordx4 v[164:167], %[vo], %[ib]\n\t"
@@ -1591,9 +1674,9 @@ __device__ __forceinline__ void prefetch_bucket(u32x32 &P, u32x32 &Q, u32x32 &il
         "global_load_dwordx4 v[220:223], %[vo], %[ib]\n\t"
         : "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[160:191]}"(ilo), "=&{v[192:223]}"(ihi), [cold] "=&v"(cold),
           [rlen] "=&v"(rlen), [roff] "=&v"(roff), [rxy] "=&v"(rxy), [qid] "=&v"(qid), [qlen] "=&v"(qlen),
-          [vo] "=&v"(vo), [sv] "=&s"(sv)
+          [vo] "+v"(vo), [sv] "=&s"(sv)
         : [cw] "v"(cw), [cv] "v"(cv), [dc] "s"(doclaim), [alen] "v"(alen), [aoff] "v"(aoff), [axy] "v"(axy),
-          [aqid] "v"(aqid), [aqlen] "v"(aqlen), [ib] "s"(ibase), [j] "v"(j)
+          [aqid] "v"(aqid), [aqlen] "v"(aqlen), [ib] "s"(ibase)
         : "memory", "scc");
 }
 
@@ -1605,9 +1688,8 @@ __device__ __forceinline__ void prefetch_bucket(u32x32 &P, u32x32 &Q, u32x32 &il
 __device__ __forceinline__ void lds_to_image_asm(uint8_t *img, uint32_t tid)
 {
     u32x32 d0, d1;
-    uint32_t vo;
+    uint32_t vo = img_vo(tid);
     asm volatile(
-        "v_lshlrev_b32 %[vo], 4, %[t]\n\t"
         "ds_read_b128 v[72:75], %[vo]\n\t"
         "ds_read_b128 v[76:79], %[vo] offset:4096\n\t"
         "ds_read_b128 v[80:83], %[vo] offset:8192\n\t"
@@ -1657,18 +1739,41 @@ __device__ __forceinline__ void lds_to_image_asm(uint8_t *img, uint32_t tid)
         "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
         "global_store_dwordx4 %[vo], v[132:135], %[img]\n\t"
         "s_nop 1\n\t"                          // store-data VGPRs: VMEM store -> VALU write hazard
-        : "=&{v[72:103]}"(d0), "=&{v[104:135]}"(d1), [vo] "=&v"(vo)
-        : [t] "v"(tid), [img] "s"(img)
+        : "=&{v[72:103]}"(d0), "=&{v[104:135]}"(d1), [vo] "+v"(vo)
+        : [img] "s"(img)
         : "memory");
 }
 
-template <bool PF, bool GR = false>
+// ZRC4_PAIR (the range form of crypt_stream_kernel): the two wave pairs of a
+// workgroup run their groups decoupled.  Pair p (waves 2p, 2p+1) owns the
+// columns with bit 7 = p, i.e. bytes [128p, 128p + 128) of every image row,
+// and moves exactly those (img_vo), so at a group boundary its waves only
+// wait for each other: they meet through an LDS counter instead of the
+// workgroup barrier.  Measured first as a timing-only ablation with whole
+// images (pair meets, outputs wrong): cfg5 284.5 -> 276.3 us, 262 144 x 1 KiB
+// 151.3 -> 148.7 (profiles/r04/ab/ab_pair.log).  0: workgroup barriers.
+#ifndef ZRC4_PAIR
+#define ZRC4_PAIR 1
+#endif
+__device__ __forceinline__ void pair_meet(uint32_t *ctr, uint32_t &gen)
+{
+    ++gen;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63u) == 0u) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+           2u * gen)
+        __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+template <bool PF, bool GR = false, bool FRAME = false>
 __global__ void __launch_bounds__(256, 2)
 crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                     const uint32_t *__restrict__ ids, uint32_t first_slot,
                     uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
                     const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
-                    uint32_t *__restrict__ err, uint8_t *__restrict__ sink, Claim cl = Claim{})
+                    uint32_t *__restrict__ err, uint8_t *__restrict__ sink, Claim cl = Claim{},
+                    FrameArgs fr = FrameArgs{})
 {
     static_assert(PF || !GR, "grouped batches run the prefetching form");
     __shared__ __attribute__((aligned(16))) uint8_t smem[GR ? kSmemStreamGr : kGroupBytes + 16];
@@ -1684,6 +1789,14 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     bool p_async = false;                     // P = next group's line 0, loaded by the line loop
 
     uint32_t w = blockIdx.x;
+#if ZRC4_PAIR
+    uint32_t *pctr = reinterpret_cast<uint32_t *>(smem + kGroupBytes) + (j >> 7);   // this pair's counter
+    uint32_t pgen = 0;                                                              // meetings so far
+    if constexpr (PF && !GR) {
+        if (j < 2u) reinterpret_cast<uint32_t *>(smem + kGroupBytes)[j] = 0u;
+        __syncthreads();
+    }
+#endif
     EntryIn cur;
     // GR: this bucket's group and whether it runs (wave-uniform), its claim
     // word's old value (lane 0 of wave 0), and the next bucket's raw entry.
@@ -1721,10 +1834,11 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     u32x32 ilo, ihi;                          // PF: this group's image, 16 x 16 B per lane
     if constexpr (PF) {
         const uint32_t g0 = GR ? gcur : (first_slot >> 8) + w;
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(arena + (size_t)g0 * kGroupBytes);
+        const uint8_t *src = arena + (size_t)g0 * kGroupBytes + img_vo(j);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const u32x4 a = src[i * 256 + j], b = src[(i + 8) * 256 + j];
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(src + i * 4096),
+                        b = *reinterpret_cast<const u32x4 *>(src + (i + 8) * 4096);
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
                 ilo[4 * i + d] = a[d];
@@ -1754,11 +1868,12 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             // younger than the prefetched image: at least the next group's
             // line-0 loads (8) and this image's stores (16)
             asm volatile("s_waitcnt vmcnt(24)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
-            u32x4 *dst = reinterpret_cast<u32x4 *>(S);
+            uint8_t *dst = S + img_vo(j);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                dst[i * 256 + j] = u32x4{ilo[4 * i], ilo[4 * i + 1], ilo[4 * i + 2], ilo[4 * i + 3]};
-                dst[(i + 8) * 256 + j] = u32x4{ihi[4 * i], ihi[4 * i + 1], ihi[4 * i + 2], ihi[4 * i + 3]};
+                *reinterpret_cast<u32x4 *>(dst + i * 4096) = u32x4{ilo[4 * i], ilo[4 * i + 1], ilo[4 * i + 2], ilo[4 * i + 3]};
+                *reinterpret_cast<u32x4 *>(dst + (i + 8) * 4096) =
+                    u32x4{ihi[4 * i], ihi[4 * i + 1], ihi[4 * i + 2], ihi[4 * i + 3]};
             }
             if constexpr (GR) {
                 // this bucket's claim (read back with the entries), and the
@@ -1766,6 +1881,9 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                 if (j == 0u) gr[kGrLost] = cur_ok && cold == cl.epoch ? 1u : 0u;
                 if (w + gridDim.x < nwg) bucket_table(gr, w + gridDim.x, qid, qlen, n, capacity, err);
             }
+#if ZRC4_PAIR
+            if constexpr (!GR) pair_meet(pctr, pgen); else
+#endif
             __syncthreads();
             if constexpr (GR) {
                 const uint32_t lost = __builtin_amdgcn_readfirstlane(gr[kGrLost]);
@@ -1912,6 +2030,9 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 
         // ---- this group's state back to HBM
         if (whole) {
+#if ZRC4_PAIR
+            if constexpr (PF && !GR) pair_meet(pctr, pgen); else
+#endif
             __syncthreads();
             lds_to_image_asm(arena + (size_t)g * kGroupBytes, j);
         } else if (!PF && active && cur.len) {
@@ -1923,11 +2044,22 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         if (!more) break;
+#if ZRC4_PAIR
+        if constexpr (PF && !GR) pair_meet(pctr, pgen); else
+#endif
         __syncthreads();      // every wave has read this image out of LDS before the next fill
         cur = nxt;
         w = wn;
         gcur = gn;
         cur_ok = nok;
+    }
+    if constexpr (FRAME) {
+        // onRecv's framing (§8f row 4) of every entry of this workgroup's
+        // chunks, raw or decrypted: every wave's payload stores have landed
+        // (same CU) before any lane reads headers back.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        frame_walk_chunks(payload, fr, blockIdx.x, gridDim.x, nwg, n, j);
     }
 #if ZRC4_TIMING
     __builtin_amdgcn_s_waitcnt(0);
@@ -2048,6 +2180,36 @@ __device__ __forceinline__ void ksa16_window_asm(uint32_t &x0, uint32_t &x1, uin
         : "memory");
 }
 
+// 32 KSA steps from a 33-byte window (q[0..7] and byte 0 of q[8]): the window
+// path's chunk for key lengths up to 32 (16c mod len + 33 <= 64 then holds
+// for 32-step chunks), half the chunk boundaries of ksa16_window_asm.
+__device__ __forceinline__ void ksa32_window_asm(uint32_t &x0, uint32_t &x1, uint32_t &a0, uint32_t &ya,
+                                                 const uint32_t (&q)[9])
+{
+    uint32_t a1, b;
+    asm volatile(
+        ZRC4_KSA_QPAIR(q0, BYTE_1, q0, BYTE_2) ZRC4_KSA_QPAIR(q0, BYTE_3, q1, BYTE_0)
+        ZRC4_KSA_QPAIR(q1, BYTE_1, q1, BYTE_2) ZRC4_KSA_QPAIR(q1, BYTE_3, q2, BYTE_0)
+        ZRC4_KSA_QPAIR(q2, BYTE_1, q2, BYTE_2) ZRC4_KSA_QPAIR(q2, BYTE_3, q3, BYTE_0)
+        ZRC4_KSA_QPAIR(q3, BYTE_1, q3, BYTE_2) ZRC4_KSA_QPAIR(q3, BYTE_3, q4, BYTE_0)
+        ZRC4_KSA_QPAIR(q4, BYTE_1, q4, BYTE_2) ZRC4_KSA_QPAIR(q4, BYTE_3, q5, BYTE_0)
+        ZRC4_KSA_QPAIR(q5, BYTE_1, q5, BYTE_2) ZRC4_KSA_QPAIR(q5, BYTE_3, q6, BYTE_0)
+        ZRC4_KSA_QPAIR(q6, BYTE_1, q6, BYTE_2) ZRC4_KSA_QPAIR(q6, BYTE_3, q7, BYTE_0)
+        ZRC4_KSA_QPAIR(q7, BYTE_1, q7, BYTE_2) ZRC4_KSA_QPAIR(q7, BYTE_3, q8, BYTE_0)
+        "s_waitcnt lgkmcnt(0)\n\t"
+        : [ya] "+v"(ya), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0), [a1] "=&v"(a1), [b] "=&v"(b)
+        : [q0] "v"(q[0]), [q1] "v"(q[1]), [q2] "v"(q[2]), [q3] "v"(q[3]), [q4] "v"(q[4]),
+          [q5] "v"(q[5]), [q6] "v"(q[6]), [q7] "v"(q[7]), [q8] "v"(q[8])
+        : "memory");
+}
+
+#ifndef ZRC4_KSA_WIN32
+#define ZRC4_KSA_WIN32 1
+#endif
+#ifndef ZRC4_KSA_EAB
+#define ZRC4_KSA_EAB 0       // timing-only: skip assembling E (outputs wrong)
+#endif
+
 // ksa_kernel's LDS: the 64 KiB S-box image, then 16 KiB of key schedule
 // prefixes (window path: dword w of lane j at kKsaSched + 4 * (w * 256 + j),
 // conflict-free for any per-lane w).  80 KiB: two workgroups per CU.
@@ -2101,38 +2263,28 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 
     // Window path (key lengths that do not divide 16 and are not 32 / 64,
     // up to kKsaWinMax): the first 64 bytes of this lane's key schedule,
-    // E[i] = key[i mod len] (rc4_encryption.h:67-70), go to LDS once, before
-    // the S-boxes are filled.  The key arrives as the <= 13 dwords that cover
-    // it (not 64 per-lane byte loads: each byte-load instruction of a wave
-    // touches ~20 cache lines), parked in the S-box area (free until the
-    // fill), and E is assembled from LDS bytes.  Layouts are transposed
-    // (dword w of lane j at 4 * (w * 256 + j)): conflict-free.
+    // E[i] = key[i mod len] (rc4_encryption.h:67-70), go to LDS once.  The key
+    // arrives as the <= 13 dwords that cover it (not 64 per-lane byte loads:
+    // each byte-load instruction of a wave touches ~20 cache lines), issued
+    // here so that their round trip overlaps the S-box fill; E is built in
+    // the lane's schedule rows with dword reads and byte aligns (~100 VALU
+    // per lane; assembling it byte by byte cost ~600 and 14 % of the KSA).
+    // Layouts are transposed (dword w of lane j at 4 * (w * 256 + j)):
+    // conflict-free.
     const bool winpath = active && kl != 0u && kl <= kKsaWinMax && !(kl <= 16u && (16u % kl) == 0u) &&
                          kl != 32u && kl != 64u;
     uint32_t *sch = reinterpret_cast<uint32_t *>(smem + kKsaSched) + j;
-    if (winpath) {
-        const uintptr_t ka = (uintptr_t)key;
-        const uint32_t *kw = reinterpret_cast<const uint32_t *>(ka & ~(uintptr_t)3);
-        const uint32_t sh = (uint32_t)(ka & 3u), nw = (sh + kl + 3u) >> 2;   // dwords overlapping the key
-        uint32_t *raw = reinterpret_cast<uint32_t *>(smem) + j;
+    // (32- and 64-byte keys take their 64-byte register pattern from the
+    // same dword loads.)
+    const bool pat64 = active && (kl == 32u || kl == 64u);
+    const uint32_t ksh = (uint32_t)((uintptr_t)key & 3u);
+    uint32_t kraw[17];
+    if (winpath || pat64) {
+        const uint32_t *kw = reinterpret_cast<const uint32_t *>((uintptr_t)key & ~(uintptr_t)3);
+        const uint32_t nw = (ksh + kl + 3u) >> 2;           // dwords overlapping the key
 #pragma unroll
-        for (uint32_t w = 0; w < 13u; ++w)
-            if (w < nw) raw[w * 256u] = kw[w];
-        const uint8_t *rb = smem + 4u * j;
-        uint32_t m = 0;
-#pragma unroll
-        for (int w = 0; w < 16; ++w) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const uint32_t p_ = sh + m;
-                v |= (uint32_t)rb[(p_ >> 2) * 1024u + (p_ & 3u)] << (8 * b);
-                if (++m == kl) m = 0;
-            }
-            sch[w * 256] = v;
-        }
+        for (uint32_t w = 0; w < 17u; ++w) kraw[w] = w < nw ? kw[w] : 0u;
     }
-    __syncthreads();                                 // the S-box area is free again
 
     // Identity boxes (:50-53): a whole, fully re-seeded group fills its 64 KiB
     // image cooperatively (row k = 256 copies of k, 16 x 16 B per lane);
@@ -2155,6 +2307,33 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             for (int k = 0; k < 256; ++k) S[(k << 8) | col] = (uint8_t)k;
     }
 
+    if (winpath && !ZRC4_KSA_EAB) {
+        // X = key || key[0..2] as aligned dwords in the schedule rows, then
+        // E dword w = X bytes r .. r+3 with r = 4w mod len (one byte align).
+        uint32_t K[12];
+#pragma unroll
+        for (int w = 0; w < 12; ++w) {
+            K[w] = __builtin_amdgcn_alignbyte(kraw[w + 1], kraw[w], ksh);
+            sch[w * 256] = K[w];                             // bytes past len: fixed below / never read
+        }
+        const uint32_t w0 = kl >> 2, m8 = 8u * (kl & 3u);
+        const uint32_t kw0 = sch[w0 * 256u];                 // the dword holding byte len (if len % 4)
+        sch[w0 * 256u] = (uint32_t)(((uint64_t)kw0 & ((1ull << m8) - 1ull)) | ((uint64_t)K[0] << m8));
+        sch[(w0 + 1u) * 256u] = (uint32_t)((uint64_t)K[0] >> (32u - m8));
+        uint32_t E[16];
+        uint32_t r = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            const uint32_t *x = sch + (r >> 2) * 256u;
+            E[w] = __builtin_amdgcn_alignbyte(x[256], x[0], r & 3u);
+            r += 4u;
+            if (r >= kl) r -= kl;
+            if (r >= kl) r -= kl;                            // len 3
+        }
+#pragma unroll
+        for (int w = 0; w < 16; ++w) sch[w * 256] = E[w];
+    }
+
     if (active && kl) {
         if (kl <= 16u && (16u % kl) == 0u) {
             // the whole key schedule (:67-70) in 16 register bytes, loaded once
@@ -2165,12 +2344,12 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             uint32_t ya = col | ((q[0] & 0xFFu) << 8);    // j = 0 + key[0] before step 0
             for (int c = 0; c < 16; ++c) ksa16_pattern_asm(x0, x1, a0, ya, q);
         } else if (kl == 32u || kl == 64u) {
-            // 32- and 64-byte keys: the schedule in 64 register bytes
+            // 32- and 64-byte keys: the schedule in 64 register bytes (the
+            // key's aligned dwords, the first 8 twice for 32 bytes)
             uint32_t q[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) q[i] = 0u;
-#pragma unroll
-            for (int u = 0; u < 64; ++u) q[u >> 2] |= (uint32_t)key[(uint32_t)u & (kl - 1u)] << (8 * (u & 3));
+            for (int i = 0; i < 16; ++i)
+                q[i] = __builtin_amdgcn_alignbyte(kraw[kl == 32u ? (i & 7) + 1 : i + 1], kraw[kl == 32u ? (i & 7) : i], ksh);
             uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col];
             uint32_t ya = col | ((q[0] & 0xFFu) << 8);
             for (int c = 0; c < 4; ++c) ksa64_pattern_asm(x0, x1, a0, ya, q);
@@ -2183,6 +2362,31 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col];
             uint32_t ya = col | ((sch[0] & 0xFFu) << 8);   // j = 0 + key[0] before step 0
             uint32_t k = 0;                                // 16c mod len
+#if ZRC4_KSA_WIN32
+            if (kl <= 32u) {
+                // 32-step chunks: 33 bytes E[k .. k+32], k = 32c mod len <= 31
+                uint32_t d[9];
+#pragma unroll
+                for (int m = 0; m < 9; ++m) d[m] = sch[m * 256];
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t sh = 8u * (k & 3u);
+                    uint32_t q[9];
+#pragma unroll
+                    for (int m = 0; m < 8; ++m)
+                        q[m] = (uint32_t)(((uint64_t)d[m + 1] << 32 | d[m]) >> sh);
+                    q[8] = d[8] >> sh;
+                    k += 32u;
+                    while (k >= kl) k -= kl;
+                    if (c < 7) {
+                        const uint32_t i0 = k >> 2;
+#pragma unroll
+                        for (int m = 0; m < 9; ++m) d[m] = sch[(i0 + m) * 256];
+                    }
+                    ksa32_window_asm(x0, x1, a0, ya, q);
+                }
+            } else
+#endif
+            {
             uint32_t d[5];
 #pragma unroll
             for (int m = 0; m < 5; ++m) d[m] = sch[m * 256];
@@ -2201,6 +2405,7 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                     for (int m = 0; m < 5; ++m) d[m] = sch[(i0 + m) * 256];
                 }
                 ksa16_window_asm(x0, x1, a0, ya, q);
+            }
             }
         } else {
             // key bytes of steps 16c .. 16c+16, fetched one chunk ahead

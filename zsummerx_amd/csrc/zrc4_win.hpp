@@ -241,7 +241,9 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
     uint64_t O = 0;
     bool valid;
     uint32_t rows[4];
-    uint32_t sxy;
+    uint32_t sxy, sxy_g;                                                   // sxy_g: kGrouped's x/y on the guess
+    unsigned long long cold = 0;                                           // kGrouped: the claim of column q (Claim)
+    bool bad = false;                                                      // kGrouped: the bucket breaks the contract
     if constexpr (MODE == kRange) {
         const uint32_t e = wg * kGroup + kb;
         ent = e;
@@ -303,8 +305,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
         for (int r = 0; r < 4; ++r)
             rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
         // x/y of the stream on the same guess (no round trip after the table build)
-        const uint32_t sxy_g = xy[gw * 256u + kb];
-        unsigned long long cold = 0;                                          // the claim of column q (Claim)
+        sxy_g = xy[gw * 256u + kb];
         if (lane == 0) cold = claim_part(cl, gw, q, wg);
         __syncthreads();
 #pragma unroll
@@ -319,11 +320,6 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             }
         }
         __syncthreads();
-        const bool lost = claim_lost(cl, ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(cold >> 32))) << 32);
-        if (fl[8] || lost) {                                                  // lost: another bucket holds column q
-            if (lane == 0) latch_fault(err, kErrGroup);
-            return;
-        }
         slot = gw * 256u + kb;
         ent = te[kb];
         valid = ent != ZRC4_INVALID;
@@ -331,20 +327,31 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             L = tl[kb];
             O = to[kb];
         }
-        sxy = valid ? sxy_g : 0u;
-        if (!__builtin_amdgcn_ballot_w64(valid)) return;
-        __syncthreads();                                                      // tables read before the ring is used
+        bad = fl[8] != 0u;
     }
     uint8_t *img = arena + (size_t)(slot >> 8) * kGroupBytes + 4u * q;
     uint8_t *msg = payload + O;
     const bool aligned = ((uintptr_t)msg & 15u) == 0u;
 
-    // payload prefetch of chunk 0 (aligned messages: whole 16-byte units)
+    // payload prefetch of chunk 0 (aligned messages: whole 16-byte units).
+    // kGrouped: issued before the claim's answer is waited for (reads of the
+    // caller's entries only; a refused bucket drops them), so its round
+    // trip overlaps the claim's instead of following it.
     uint4 pre[kWinUnits];
 #pragma unroll
     for (uint32_t u = 0; u < kWinUnits; ++u) {
         const uint32_t pos = 16u * (l + kWinLanes * u);
         if (aligned && pos + 16u <= L) pre[u] = *reinterpret_cast<const uint4 *>(msg + pos);
+    }
+    if constexpr (MODE == kGrouped) {
+        const bool lost = claim_lost(cl, ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(cold >> 32))) << 32);
+        if (bad || lost) {                                                    // lost: another bucket holds column q
+            if (lane == 0) latch_fault(err, kErrGroup);
+            return;
+        }
+        sxy = valid ? sxy_g : 0u;
+        if (!__builtin_amdgcn_ballot_w64(valid)) return;
+        __syncthreads();                                                      // tables read before the ring is used
     }
 
     uint8_t *S = Sb + b * 256u;
