@@ -104,6 +104,9 @@ def main():
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--define", action="append", default=[], help="extra -D for the timing build (NAME=V)")
     ap.add_argument("--dump", default="", help="save the raw per-workgroup stamps (npz) under this prefix")
+    ap.add_argument("--ids", choices=("range", "grouped"), default="range",
+                    help="grouped: zrc4_crypt_grouped, slots permuted inside each group and groups in random order "
+                         "(bench.py --ids grouped)")
     args = ap.parse_args()
     from zsummerx_amd import build
     defs = {"ZRC4_TIMING": "1"}
@@ -133,6 +136,18 @@ def main():
         pay = torch.from_numpy(synth.payload(0, n * L, threads=8)).to(dev)
         off = torch.arange(n, dtype=torch.int64, device=dev) * L
         ln = torch.full((n,), L, dtype=torch.int32, device=dev)
+        gids = None
+        if args.ids == "grouped":
+            rng = np.random.default_rng(77)
+            perm = np.empty(n, dtype=np.int64)
+            for b in range(R):
+                pos = 0
+                for g in rng.permutation(-(-S // 256)):
+                    lo, hi = b * S + g * 256, min(b * S + (g + 1) * 256, (b + 1) * S)
+                    perm[b * S + pos: b * S + pos + (hi - lo)] = lo + rng.permutation(hi - lo)
+                    pos += hi - lo
+            gids = torch.from_numpy(perm.astype(np.int32)).to(dev)
+            off = torch.from_numpy(perm * L).to(dev)
         h = C.c_void_p()
         _capi.check(lib.zrc4_create(C.byref(h), 0, n), "create")
         _capi.check(lib.zrc4_ksa_range(h, 0, C.c_void_p(keys.data_ptr()), C.c_void_p(koff.data_ptr()),
@@ -142,9 +157,14 @@ def main():
             b = i % R
             if i == args.launches - 1:
                 ev0.record()
-            _capi.check(lib.zrc4_crypt_range(h, b * S, C.c_void_p(pay.data_ptr()),
-                                             C.c_void_p(off.data_ptr() + 8 * b * S),
-                                             C.c_void_p(ln.data_ptr() + 4 * b * S), S, st))
+            if gids is None:
+                _capi.check(lib.zrc4_crypt_range(h, b * S, C.c_void_p(pay.data_ptr()),
+                                                 C.c_void_p(off.data_ptr() + 8 * b * S),
+                                                 C.c_void_p(ln.data_ptr() + 4 * b * S), S, st))
+            else:
+                _capi.check(lib.zrc4_crypt_grouped(h, C.c_void_p(gids.data_ptr() + 4 * b * S),
+                                                   C.c_void_p(pay.data_ptr()), C.c_void_p(off.data_ptr() + 8 * b * S),
+                                                   C.c_void_p(ln.data_ptr() + 4 * b * S), S, st))
         ev1.record()
         _capi.check(lib.zrc4_sync(h, st))
         torch.cuda.synchronize()
@@ -161,6 +181,7 @@ def main():
         groups = -(-S // 256)
         wgs = min(groups, 512)
         out[wl] = summarise(rt, clk, wgs, min(7, groups // wgs))
+        out[wl]["ids"] = args.ids
         out[wl]["last_launch_event_us"] = round(last_event_us, 2)
         out[wl]["by_place"] = by_place(rt, hwid, wgs, min(7, groups // wgs))
         print(wl, json.dumps(out[wl]), flush=True)

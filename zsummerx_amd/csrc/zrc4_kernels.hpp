@@ -1582,14 +1582,16 @@ struct BucketView {
 
 // After the barrier that follows bucket_table(nb): the votes and this lane's
 // table entry.  A refused bucket latches kErrGroup (thread 0).
+template <int NW = 4>
 __device__ __forceinline__ BucketView bucket_read(const uint32_t *gr, uint32_t nb, uint32_t *err)
 {
-    const uint4 va = *reinterpret_cast<const uint4 *>(gr + kGrVote), vb = *reinterpret_cast<const uint4 *>(gr + kGrVote + 4);
+    const uint4 va = *reinterpret_cast<const uint4 *>(gr + kGrVote);
+    const uint4 vb = NW > 2 ? *reinterpret_cast<const uint4 *>(gr + kGrVote + 4) : make_uint4(0u, 0u, 0u, 0u);
     const uint32_t vote[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
     uint32_t g = ZRC4_INVALID;
     bool bad = false;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
         const uint32_t gw = __builtin_amdgcn_readfirstlane(vote[2 * w]);
         bad = bad || __builtin_amdgcn_readfirstlane(vote[2 * w + 1]) != 0u;
         if (gw != ZRC4_INVALID) {
@@ -1599,7 +1601,7 @@ __device__ __forceinline__ BucketView bucket_read(const uint32_t *gr, uint32_t n
     }
     BucketView bv;
     bv.ok = g != ZRC4_INVALID && !bad;
-    if (g != ZRC4_INVALID && bad && threadIdx.x == 0u) latch_fault(err, kErrGroup);
+    if (g != ZRC4_INVALID && bad && (threadIdx.x & (NW * 64u - 1u)) == 0u) latch_fault(err, kErrGroup);
     const uint32_t t = gr[kGrTab + threadIdx.x];
     bv.valid = bv.ok && (t >> 8) == nb;
     bv.g = bv.ok ? g : 0u;
@@ -1607,6 +1609,128 @@ __device__ __forceinline__ BucketView bucket_read(const uint32_t *gr, uint32_t n
     return bv;
 }
 
+// Grouped buckets with wave pairs (ZRC4_PAIR): each pair (waves 2p, 2p+1)
+// runs its half of every bucket on its own schedule, so it keeps its own
+// votes / claim-lost word / table (region p, kGrPairWords words), claims
+// its own part p of the group (so two buckets naming one group can only
+// split it by halves, each slot still all or nothing), and builds the table
+// of the next bucket from all 256 raw entries: its own lanes' and the other
+// pair's, which both pairs publish into an LDS staging buffer one boundary
+// ahead (the raw entries are loaded three buckets ahead instead of two).  A
+// pair only ever waits for the other to have finished the previous
+// boundary -- the staging double buffer's condition -- which a pair never
+// a whole group behind does not trigger.
+constexpr uint32_t kGrPairCnt = kGrTab + 256u;            // 2 x 256 slot counts (boundary parity)
+constexpr uint32_t kGrPairWords = kGrPairCnt + 512u;      // votes, lost, table, counts
+constexpr uint32_t kGrMeet = 2u * kGrPairWords;           // 2 pair-meet counters
+constexpr uint32_t kGrCnt = kGrMeet + 2u;                 // 2 boundaries-done counters
+constexpr uint32_t kGrStg = kGrCnt + 2u;                  // 2 x 256 raw entries {id, len}
+constexpr uint32_t kSmemStreamGrPair = kGroupBytes + 4u * (kGrStg + 1024u);   // 75 920 B: two workgroups per CU
+
+// Pair version of the bucket table, in two halves around the pair's meet
+// so that a boundary pays two LDS round trips (each one queues behind the
+// other workgroup's keystream on the CU's LDS) and holds no entry in
+// registers across the meet:
+//   bucket_table_pair (before the meet): each wave reads ALL 256 raw entries
+//     of bucket nb from staging (lane l: l, l+64, l+128, l+192) and votes
+//     the group (first busy id) and "a busy entry of another group" by
+//     itself -- both waves reach the same answer, nothing to exchange; for
+//     its half of the entries it writes the table (slot -> entry) and adds 1
+//     to the slot's count (boundary parity cnt, zeroed one boundary ahead);
+//   bucket_read_pair (after the meet): a count above 1 anywhere is a slot
+//     named twice (each wave reads all 256), plus this lane's own slot.
+struct PairVote {
+    uint32_t guess;      // the bucket's group (first busy id), or ZRC4_INVALID
+    bool bad;            // a busy entry of another group
+};
+
+// ocnt / bk: the staging buffer is read only once the other pair has
+// finished boundary bk - 1 (its counter read first, in the same round trip).
+__device__ __forceinline__ PairVote bucket_table_pair(uint32_t *grp, const uint32_t *stg, uint32_t nb,
+                                                      uint32_t capacity, uint32_t *err, const uint32_t *ocnt,
+                                                      uint32_t bk)
+{
+    // (the lane's addresses are recomputed per boundary, not hoisted out of
+    // the persistent loop into registers that would be live across it)
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const uint32_t l = tid & 63u, wv = __builtin_amdgcn_readfirstlane((tid >> 6) & 1u);
+    uint32_t *cnt = grp + kGrPairCnt + 256u * (bk & 1u);
+    uint32_t *nxt = grp + kGrPairCnt + 256u * ((bk + 1u) & 1u);
+    uint2 r[4];
+    const uint32_t c = __hip_atomic_load(ocnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int m = 0; m < 4; ++m) r[m] = *reinterpret_cast<const uint2 *>(stg + 2u * (l + 64u * m));
+    if (__builtin_amdgcn_readfirstlane(c) < bk) {            // the other pair is a whole group behind
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ocnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < bk)
+            __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int m = 0; m < 4; ++m) r[m] = *reinterpret_cast<const uint2 *>(stg + 2u * (l + 64u * m));
+    }
+    PairVote pv;
+    pv.guess = ZRC4_INVALID;
+    uint32_t id[4];
+    bool busy[4];
+#pragma unroll
+    for (int m = 3; m >= 0; --m) {
+        id[m] = r[m].x;
+        if (id[m] >= capacity && id[m] != ZRC4_INVALID) {      // ZRC4_IDLE_SLOT pads buckets
+            latch_fault(err, kErrSlotRange);
+            id[m] = ZRC4_INVALID;
+        }
+        busy[m] = id[m] != ZRC4_INVALID && r[m].y != 0u;
+        const uint64_t bm = __ballot(busy[m]);
+        if (bm) pv.guess = __builtin_amdgcn_readlane(id[m], (int)__builtin_ctzll(bm)) >> 8;
+    }
+    bool badl = false;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        badl = badl || (busy[m] && (id[m] >> 8) != pv.guess);
+        if (busy[m] && (uint32_t)(m >> 1) == wv) {
+            grp[kGrTab + (id[m] & 255u)] = nb * kGroup + l + 64u * m;
+            __hip_atomic_fetch_add(cnt + (id[m] & 255u), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    nxt[wv * 128u + l] = 0u;
+    nxt[wv * 128u + 64u + l] = 0u;
+    pv.bad = __ballot(badl) != 0u;
+    if (l == 0u) {                                           // kept in LDS, not in registers, across the meet
+        grp[kGrVote + 2u * wv] = pv.guess;
+        grp[kGrVote + 2u * wv + 1u] = pv.bad ? 1u : 0u;
+    }
+    return pv;
+}
+
+// cnt: the counts of the boundary that built nb's table.
+__device__ __forceinline__ BucketView bucket_read_pair(const uint32_t *grp, const uint32_t *cnt, uint32_t nb,
+                                                       uint32_t *err)
+{
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const uint32_t l = tid & 63u, wv = __builtin_amdgcn_readfirstlane((tid >> 6) & 1u);
+    const uint2 vote = *reinterpret_cast<const uint2 *>(grp + kGrVote + 2u * wv);
+    PairVote pv;
+    pv.guess = __builtin_amdgcn_readfirstlane(vote.x);
+    pv.bad = __builtin_amdgcn_readfirstlane(vote.y) != 0u;
+    uint32_t most = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) most = max(most, cnt[l + 64u * m]);
+    const uint32_t t = grp[kGrTab + tid];
+    const bool bad = pv.bad || __ballot(most > 1u) != 0u;
+    BucketView bv;
+    bv.ok = pv.guess != ZRC4_INVALID && !bad;
+    if (pv.guess != ZRC4_INVALID && bad && (threadIdx.x & 127u) == 0u) latch_fault(err, kErrGroup);
+    bv.valid = bv.ok && (t >> 8) == nb;
+    bv.g = bv.ok ? pv.guess : 0u;
+    bv.ent = bv.valid ? t : nb * kGroup;
+    return bv;
+}
+
+#ifndef ZRC4_GR_CLAIM_AB
+#define ZRC4_GR_CLAIM_AB 0       // timing-only claim forms (1: atomic without return, 2: plain store)
+#endif
 // The next bucket's claim (lane 0 of wave 0 swaps the launch epoch into the
 // high half of the group's part-0 claim word -- only the epoch decides a
 // claim -- and every other wave reads that half instead, so every wave issues
@@ -1630,7 +1754,13 @@ __device__ __forceinline__ void prefetch_bucket(u32x32 &P, u32x32 &Q, u32x32 &il
         "s_mov_b64 exec, 1\n\t"
         "s_cmp_eq_u32 %[dc], 0\n\t"
         "s_cbranch_scc1 PB_READ_%=\n\t"
+#if ZRC4_GR_CLAIM_AB == 1
+        "global_atomic_swap %[cw], %[cv], off\n\t"      // timing-only: no return
+#elif ZRC4_GR_CLAIM_AB == 2
+        "global_store_dword %[cw], %[cv], off\n\t"      // timing-only: a plain store
+#else
         "global_atomic_swap %[cold], %[cw], %[cv], off sc0\n\t"
+#endif
         "s_branch PB_CLAIMED_%=\n\t"
         "PB_READ_%=:\n\t"
         "global_load_dword %[cold], %[cw], off\n\t"
@@ -1776,7 +1906,8 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                     FrameArgs fr = FrameArgs{})
 {
     static_assert(PF || !GR, "grouped batches run the prefetching form");
-    __shared__ __attribute__((aligned(16))) uint8_t smem[GR ? kSmemStreamGr : kGroupBytes + 16];
+    constexpr bool PG = GR && ZRC4_PAIR;       // grouped buckets by wave pairs
+    __shared__ __attribute__((aligned(16))) uint8_t smem[GR ? (PG ? kSmemStreamGrPair : kSmemStreamGr) : kGroupBytes + 16];
     uint8_t *S = smem;
     if (!lds_base_ok(S, err)) return;
     uint32_t *gr = reinterpret_cast<uint32_t *>(smem + kGroupBytes);    // GR: votes, claim word, table
@@ -1789,22 +1920,75 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     bool p_async = false;                     // P = next group's line 0, loaded by the line loop
 
     uint32_t w = blockIdx.x;
+    const uint32_t pr = __builtin_amdgcn_readfirstlane(j >> 7);   // this wave's pair (an SGPR)
 #if ZRC4_PAIR
-    uint32_t *pctr = reinterpret_cast<uint32_t *>(smem + kGroupBytes) + (j >> 7);   // this pair's counter
-    uint32_t pgen = 0;                                                              // meetings so far
+    uint32_t *pctr = gr + (GR ? kGrMeet : 0u) + pr;         // this pair's meet counter
+    uint32_t pgen = 0;                                      // meetings so far
     if constexpr (PF && !GR) {
-        if (j < 2u) reinterpret_cast<uint32_t *>(smem + kGroupBytes)[j] = 0u;
+        if (j < 2u) gr[j] = 0u;
         __syncthreads();
     }
 #endif
+    // PG: this pair's region, the staging buffers, boundaries done so far;
+    // the next bucket's vote (before the meet) and view (after it)
+    uint32_t *grp = gr + (PG ? pr * kGrPairWords : 0u);
+    uint32_t bk = 0;
     EntryIn cur;
+    u32x32 ilo, ihi;                          // PF: this group's image, 16 x 16 B per lane
+    auto load_image = [&](uint32_t g0) {
+        const uint8_t *src = arena + (size_t)g0 * kGroupBytes + img_vo(j);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(src + i * 4096),
+                        b = *reinterpret_cast<const u32x4 *>(src + (i + 8) * 4096);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                ilo[4 * i + d] = a[d];
+                ihi[4 * i + d] = b[d];
+            }
+        }
+    };
     // GR: this bucket's group and whether it runs (wave-uniform), its claim
     // word's old value (lane 0 of wave 0), and the next bucket's raw entry.
     uint32_t gcur = 0;
     bool cur_ok = false;
     uint32_t cold = 0;
     uint32_t qid = ZRC4_INVALID, qlen = 0;
-    if constexpr (GR) {
+    if constexpr (PG) {
+        // Prologue (whole workgroup): bucket w's table in pair 0's region,
+        // each pair's claim on its part, the permuted entry, x/y and image;
+        // bucket w + grid's raw entries into staging buffer 1 (the table of
+        // boundary 0), bucket w + 2 grid's into qid / qlen (published at
+        // boundary 0).
+        gr[kGrTab + j] = ZRC4_INVALID;
+        gr[kGrPairWords + kGrTab + j] = ZRC4_INVALID;
+#pragma unroll
+        for (uint32_t c = 0; c < 4u; ++c) gr[(c >> 1) * kGrPairWords + kGrPairCnt + 256u * (c & 1u) + j] = 0u;
+        if (j < 4u) gr[kGrMeet + j] = 0u;
+        const uint32_t e0 = w * kGroup + j, e1 = (w + gridDim.x) * kGroup + j, e2 = e1 + gridDim.x * kGroup;
+        const uint32_t id0 = e0 < n ? ids[e0] : ZRC4_INVALID, l0 = e0 < n ? len[e0] : 0u;
+        const uint32_t id1 = e1 < n ? ids[e1] : ZRC4_INVALID, l1 = e1 < n ? len[e1] : 0u;
+        if (e2 < n) {
+            qid = ids[e2];
+            qlen = len[e2];
+        }
+        *reinterpret_cast<uint2 *>(gr + kGrStg + 512u + 2u * j) = make_uint2(id1, l1);
+        __syncthreads();
+        bucket_table(gr, w, id0, l0, n, capacity, err);
+        __syncthreads();
+        const BucketView bv = bucket_read(gr, w, err);
+        gcur = bv.g;
+        cur_ok = bv.ok;
+        if (bv.ok && (j & 127u) == 0u)
+            cold = __hip_atomic_exchange(reinterpret_cast<uint32_t *>(cl.word + (size_t)bv.g * kClaimParts + (j >> 7)) + 1,
+                                         cl.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cur.len = bv.valid ? len[bv.ent] : 0u;
+        cur.off = bv.valid ? off[bv.ent] : 0u;
+        cur.slot = bv.valid ? bv.g * 256u + j : ZRC4_INVALID;
+        cur.xy = xy[bv.g * 256u + j];
+        load_image(gcur);                     // with the entry gathers, not after the barrier
+        __syncthreads();                      // table and votes read before the pairs build their own
+    } else if constexpr (GR) {
         // Prologue: bucket w's table (compiler loads, waited for once below),
         // its claim, permuted entry, x/y and image; bucket w + grid's raw entry.
         gr[kGrTab + j] = ZRC4_INVALID;
@@ -1827,25 +2011,12 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         cur.off = bv.valid ? off[bv.ent] : 0u;
         cur.slot = bv.valid ? bv.g * 256u + j : ZRC4_INVALID;
         cur.xy = xy[bv.g * 256u + j];
+        load_image(gcur);                     // with the entry gathers, not after the barrier
         __syncthreads();                      // table and votes read before the next bucket's are built
     } else {
         load_entry(cur, w, j, ids, first_slot, off, len, n, capacity, err, xy);
     }
-    u32x32 ilo, ihi;                          // PF: this group's image, 16 x 16 B per lane
-    if constexpr (PF) {
-        const uint32_t g0 = GR ? gcur : (first_slot >> 8) + w;
-        const uint8_t *src = arena + (size_t)g0 * kGroupBytes + img_vo(j);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const u32x4 a = *reinterpret_cast<const u32x4 *>(src + i * 4096),
-                        b = *reinterpret_cast<const u32x4 *>(src + (i + 8) * 4096);
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                ilo[4 * i + d] = a[d];
-                ihi[4 * i + d] = b[d];
-            }
-        }
-    }
+    if constexpr (PF && !GR) load_image((first_slot >> 8) + w);
     LineSetup ls;
     line_setup(ls, payload + cur.off, cur.len);
     u32x32 P, Q = {};
@@ -1868,6 +2039,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             // younger than the prefetched image: at least the next group's
             // line-0 loads (8) and this image's stores (16)
             asm volatile("s_waitcnt vmcnt(24)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
+            if (k_t == 1u) stream_stamp(sink, 9);    // ZRC4_TIMING: boundary 0, next image in
             uint8_t *dst = S + img_vo(j);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -1875,21 +2047,47 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                 *reinterpret_cast<u32x4 *>(dst + (i + 8) * 4096) =
                     u32x4{ihi[4 * i], ihi[4 * i + 1], ihi[4 * i + 2], ihi[4 * i + 3]};
             }
-            if constexpr (GR) {
+            asm volatile("" ::: "memory");        // the image is in LDS (its registers free) before the tables
+            if constexpr (PG) {
+                // this pair's claim on the bucket; the next bucket's table
+                // from both pairs' raw entries (staging (bk + 1) & 1) once the
+                // other pair has finished boundary bk - 1, then bucket
+                // w + 2 grid's raw entries published (staging bk & 1)
+                if ((j & 127u) == 0u) grp[kGrLost] = cur_ok && cold == cl.epoch ? 1u : 0u;
+                if (w + gridDim.x < nwg)
+                    (void)bucket_table_pair(grp, gr + kGrStg + 512u * ((bk + 1u) & 1u), w + gridDim.x, capacity, err,
+                                            gr + kGrCnt + (pr ^ 1u), bk);
+                else
+                    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(gr + kGrCnt + (pr ^ 1u), __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) < bk)
+                        __builtin_amdgcn_s_sleep(1);
+                asm volatile("" ::: "memory");
+                const bool qv = (w + 2u * gridDim.x) * kGroup + j < n;
+                *reinterpret_cast<uint2 *>(gr + kGrStg + 512u * (bk & 1u) + 2u * j) =
+                    make_uint2(qv ? qid : ZRC4_INVALID, qlen);
+            } else if constexpr (GR) {
                 // this bucket's claim (read back with the entries), and the
                 // table of the bucket after next from its raw entries
                 if (j == 0u) gr[kGrLost] = cur_ok && cold == cl.epoch ? 1u : 0u;
                 if (w + gridDim.x < nwg) bucket_table(gr, w + gridDim.x, qid, qlen, n, capacity, err);
             }
 #if ZRC4_PAIR
-            if constexpr (!GR) pair_meet(pctr, pgen); else
+            if constexpr (!GR || PG) pair_meet(pctr, pgen); else
 #endif
             __syncthreads();
+            uint32_t lostv = 0;
+            if constexpr (PG) {
+                // both waves are past their staging accesses of boundary bk
+                if ((j & 127u) == 0u)
+                    __hip_atomic_fetch_add(gr + kGrCnt + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                ++bk;
+                lostv = __builtin_amdgcn_readfirstlane(grp[kGrLost]);
+            }
             if constexpr (GR) {
-                const uint32_t lost = __builtin_amdgcn_readfirstlane(gr[kGrLost]);
+                const uint32_t lost = PG ? lostv : __builtin_amdgcn_readfirstlane(grp[kGrLost]);
                 if (cur_ok && lost != 0u) {
                     // another bucket of this launch holds the group: skip this one whole
-                    if (j == 0u) latch_fault(err, kErrGroup);
+                    if ((j & (PG ? 127u : 255u)) == 0u) latch_fault(err, kErrGroup);
                     cur_ok = false;
                     whole = false;
                     cur.len = 0u;
@@ -1944,15 +2142,26 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #endif
         p_async = false;
         if (ls.wmax > 2u) issue_line1_asm(Q, ls, sk);
+        if (k_t == 1u) stream_stamp(sink, 11);       // ZRC4_TIMING: boundary 0, tables read / met
         if constexpr (GR) {
             if (more) {
-                const BucketView bv = bucket_read(gr, wn, err);
+                const BucketView bv = PG ? bucket_read_pair(grp, grp + kGrPairCnt + 256u * ((bk - 1u) & 1u), wn, err)
+                                         : bucket_read(gr, wn, err);
+                if (k_t == 1u) stream_stamp(sink, 10);   // ZRC4_TIMING: boundary 0, next bucket's view read
                 gn = bv.g;
                 nok = bv.ok;
-                const uint32_t eq = (wn + gridDim.x) * kGroup + j < n ? (wn + gridDim.x) * kGroup + j : n - 1u;
-                const uint32_t dc = __builtin_amdgcn_readfirstlane(nok && j < 64u ? 1u : 0u);
+                // raw entries of the bucket after next (PG: two after next)
+                const uint32_t ea = (wn + (PG ? 2u : 1u) * gridDim.x) * kGroup + j;
+                const uint32_t eq = ea < n ? ea : n - 1u;
+                // the claim: wave 0 (PG: the first wave of each pair) swaps
+#ifndef ZRC4_GR_NOSWAP_AB
+#define ZRC4_GR_NOSWAP_AB 0      // timing-only: the claim word read, never swapped (claims off)
+#endif
+                const uint32_t dc = __builtin_amdgcn_readfirstlane(
+                    !ZRC4_GR_NOSWAP_AB && nok && (j & (PG ? 127u : 255u)) < 64u ? 1u : 0u);
                 prefetch_bucket(P, Q, ilo, ihi, cold, rlen, roff, rxy, qid, qlen,
-                                reinterpret_cast<const uint32_t *>(cl.word + (size_t)gn * kClaimParts) + 1, cl.epoch,
+                                reinterpret_cast<const uint32_t *>(cl.word + (size_t)gn * kClaimParts + (PG ? pr : 0u)) + 1,
+                                cl.epoch,
                                 dc, bv.valid ? len + bv.ent : cl.zero,
                                 bv.valid ? off + bv.ent : reinterpret_cast<const uint64_t *>(cl.zero),
                                 xy + gn * 256u + j, ids + eq, len + eq, arena + (size_t)gn * kGroupBytes, j);
@@ -2018,6 +2227,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             }
             // the loop's last two halves issue no loads, so P/Q are free again
             line_setup(ls, payload + nxt.off, nxt.len);
+            if (k_t == 1u) stream_stamp(sink, 12);   // ZRC4_TIMING: boundary 0, next entries in
             if (!p_async) {
 #if ZRC4_LINE0_ASM
                 if constexpr (PF) issue_line0_asm(P, ls, sk);
@@ -2031,10 +2241,11 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         // ---- this group's state back to HBM
         if (whole) {
 #if ZRC4_PAIR
-            if constexpr (PF && !GR) pair_meet(pctr, pgen); else
+            if constexpr (PF && (!GR || PG)) pair_meet(pctr, pgen); else
 #endif
             __syncthreads();
             lds_to_image_asm(arena + (size_t)g * kGroupBytes, j);
+            if (k_t == 1u) stream_stamp(sink, 13);   // ZRC4_TIMING: boundary 0, image out
         } else if (!PF && active && cur.len) {
             scatter_column(arena, cur.slot, S, col);
         } else if (GR) {
@@ -2045,7 +2256,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         }
         if (!more) break;
 #if ZRC4_PAIR
-        if constexpr (PF && !GR) pair_meet(pctr, pgen); else
+        if constexpr (PF && (!GR || PG)) pair_meet(pctr, pgen); else
 #endif
         __syncthreads();      // every wave has read this image out of LDS before the next fill
         cur = nxt;
