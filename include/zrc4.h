@@ -192,11 +192,12 @@ int zrc4_frame_scan(zrc4_ctx *ctx, const uint8_t *buf, const uint64_t *off,
  * semantics for the crypt, then for every entry i the zrc4_frame_scan walk of
  * payload[frame->off[i] .. frame->off[i] + frame->len[i]) (the whole receive
  * block, which may start before the decrypted tail) into npk/used/status/
- * pkt_len[i] exactly as zrc4_frame_scan defines them.  In the chain-bound
- * regime (at most one slot group per CU) each lane frames its own session in
- * the crypt kernel's epilogue; larger batches run the throughput kernel and
- * the scan as a second launch.  Outputs of a bucket refused with
- * ZRC4_ERR_GROUP are unspecified.  Device pointers; asynchronous. */
+ * pkt_len[i] exactly as zrc4_frame_scan defines them.  One launch at every
+ * size: in the chain-bound regime (at most one slot group per CU) each lane
+ * frames its own session in the crypt kernel's epilogue; larger batches run
+ * the persistent throughput kernel, whose workgroups frame the entries of the
+ * 256-entry chunks they decrypted in their tail.  Outputs of a bucket refused
+ * with ZRC4_ERR_GROUP are unspecified.  Device pointers; asynchronous. */
 typedef struct zrc4_frame_args {
     const uint64_t *off;
     const uint32_t *len;

@@ -335,8 +335,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
 
     // payload prefetch of chunk 0 (aligned messages: whole 16-byte units).
     // kGrouped: issued before the claim's answer is waited for (reads of the
-    // caller's entries only; a refused bucket drops them), so its round
-    // trip overlaps the claim's instead of following it.
+    // caller's entries only; a refused bucket drops them).
     uint4 pre[kWinUnits];
 #pragma unroll
     for (uint32_t u = 0; u < kWinUnits; ++u) {
@@ -344,8 +343,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
         if (aligned && pos + 16u <= L) pre[u] = *reinterpret_cast<const uint4 *>(msg + pos);
     }
     if constexpr (MODE == kGrouped) {
-        const bool lost = claim_lost(cl, ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(cold >> 32))) << 32);
-        if (bad || lost) {                                                    // lost: another bucket holds column q
+        if (bad) {
             if (lane == 0) latch_fault(err, kErrGroup);
             return;
         }
@@ -385,6 +383,17 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             w.v = (1u << 8) | (255u - l);
         }
         win_windows(w, rem, l, sb, mb, rb);
+        if constexpr (MODE == kGrouped) {
+            // The claim's answer is first needed here: nothing has been
+            // written yet (the windows run in LDS), so its round trip hides
+            // under the first chunk's keystream.  lost: another bucket of
+            // this launch holds column q; store nothing.
+            if (c0 == 0u &&
+                claim_lost(cl, ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(cold >> 32))) << 32)) {
+                if (lane == 0) latch_fault(err, kErrGroup);
+                return;
+            }
+        }
         // XOR pass of [c0, c1): whole 16-byte units from the prefetch, bytes
         // otherwise (streams already past their end skip it: c1 - c0 would wrap)
         if (c0 >= L) {
