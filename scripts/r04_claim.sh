@@ -14,11 +14,8 @@ step() {  # name, seconds, command...
     echo "[$name] rc=$rc"; grep -v amdgpu.ids "$OUT/$name.log" | tail -${TAILN:-3} | cut -c1-700
     if [ $rc -ne 0 ]; then echo "[$name] failed: stopping GPU work in this call"; exit $rc; fi
 }
-TAILN=3 step tests 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread \
-    -p no:cacheprovider -k "grouped or window"
-step ab_win 600 python tools/ab_bench.py --variant new: --variant c2@c4aa2a0: --ids grouped --workloads cfg2,16384x1024 \
-    --rounds 9 --launches 20
-step ab_claim 1200 python tools/ab_bench.py --variant new: --variant last:ZRC4_GR_CLAIM_LAST=1 --variant nr:ZRC4_GR_CLAIM_AB=1 \
-    --variant st:ZRC4_GR_CLAIM_AB=2 --variant noswap:ZRC4_GR_NOSWAP_AB=1 --no-check --ids grouped --workloads cfg5 \
-    --rounds 7 --launches 30
+TAILN=3 step tests 900 python -u -m pytest tests/test_gpu_parity.py tests/test_frame_scan.py -m gpu -x -q --timeout 300 --timeout-method thread \
+    -p no:cacheprovider -k "grouped or window or fused"
+step ab_claim 1200 python tools/ab_bench.py --variant new: --variant pc0:ZRC4_GR_PRECLAIM=0 \
+    --ids grouped --workloads cfg5,262144x1024,131072x1024 --rounds 7 --launches 30
 echo r04 claim done

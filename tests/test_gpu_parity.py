@@ -607,8 +607,9 @@ def test_grouped_ids_mixed_bucket_is_refused(built, torch_cuda):
         assert got[256 * 32: 257 * 32].tobytes() == ks
 
 
-@pytest.mark.parametrize("nb", [20, 100, 200, 700])
-def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb):
+@pytest.mark.parametrize("nb,variant", [(20, None), (100, None), (200, None), (700, None), (1600, None),
+                                        (1600, "preclaim1")])
+def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb, variant):
     """The cross-bucket half of the zrc4_crypt_grouped contract: two buckets
     of one call name the same group (disjoint slots of it).  The call reports
     ZRC4_ERR_GROUP; every other bucket is bit-exact (payload and states); in
@@ -616,7 +617,11 @@ def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb):
     the oracle does with its state advanced, or untouched with its state
     unchanged -- never raced.  nb = 20: the window kernel (one claim per
     dword column), 100: half-group workgroups, 200: whole-group workgroups,
-    700: the persistent kernel (one claim per bucket, taken a group ahead)."""
+    700 / 1600: the persistent kernel (each pair claims its half of every
+    bucket's group a group ahead; from 3 buckets per workgroup (1600) the
+    first 64 of a workgroup in its prologue instead -- the preclaim1 test
+    build pre-claims only the first, so the contested buckets meet across
+    both paths).  At 1600 buckets every 5th uncontested entry is checked."""
     torch = torch_cuda
     from zsummerx_amd._capi import IDLE_SLOT
     rng = np.random.default_rng(500 + nb)
@@ -647,7 +652,8 @@ def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb):
     L = np.where(busy, rng.integers(1, 500, ids.size), 0).astype(np.uint32)
     off = np.arange(ids.size, dtype=np.uint64) * 512
     data = rng.integers(0, 256, ids.size * 512, dtype=np.uint8)
-    with Context(0, cap) as c:
+    from zsummerx_amd import build
+    with Context(0, cap, lib=None if variant is None else build.PKG / f"libzrc4_{variant}.so") as c:
         c.ksa_range(0, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
         pay = T(data)
         c.crypt_grouped(pay, T(off.view(np.int64)), T(L.view(np.int32)), T(ids.view(np.int32)), stream=s)
@@ -658,6 +664,8 @@ def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb):
         crypted = untouched = 0
         for e in np.flatnonzero(busy):
             slot, a, z = int(ids[e]), int(off[e]), int(off[e] + L[e])
+            if nb > 1000 and slot // 256 != contested and e % 5:
+                continue
             before = ob.state(slot)
             want = data[a:z].copy()
             st = ob.st[slot]
@@ -680,7 +688,8 @@ def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb):
         assert untouched >= 1 and crypted + untouched == 256
 
 
-def test_grouped_stream_refusals(built, torch_cuda):
+@pytest.mark.parametrize("variant", [None, "preclaim1"])
+def test_grouped_stream_refusals(built, torch_cuda, variant):
     """The persistent kernel's grouped form (600 buckets > 256 CUs) with every
     refusal at once: a bucket whose busy entries span two groups, a bucket
     naming one slot twice, a bucket with an id past the arena (that entry is
@@ -688,7 +697,8 @@ def test_grouped_stream_refusals(built, torch_cuda):
     and a slot listed twice with length 0 once (not busy: allowed).  The call
     reports ZRC4_ERR_GROUP; refused buckets leave payload and states
     untouched; every other entry is bit-exact against the oracle.  A second
-    call afterwards (no faults) continues every keystream."""
+    call afterwards (no faults) continues every keystream.  preclaim1: the
+    test build whose workgroups claim only their first bucket up front."""
     torch = torch_cuda
     from zsummerx_amd._capi import IDLE_SLOT
     rng = np.random.default_rng(77)
@@ -703,7 +713,8 @@ def test_grouped_stream_refusals(built, torch_cuda):
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     s = torch.cuda.current_stream()
     mixed, twice, past, zero_dup = 5, 301, 450, 77
-    with Context(0, cap) as c:
+    from zsummerx_amd import build
+    with Context(0, cap, lib=None if variant is None else build.PKG / f"libzrc4_{variant}.so") as c:
         c.ksa_range(0, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
         for call in range(2):
             ids = grouped_batch(rng, nb, G, (2, 256))

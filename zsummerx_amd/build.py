@@ -212,7 +212,8 @@ def build_oracle() -> None:
 # A/B builds the GPU tests load (tests/test_gpu_parity.py): built with the
 # product so that no test compiles on the GPU box.
 TEST_VARIANTS = {"wintag4": {"ZRC4_WIN_TAG_LIMIT": 4},
-                 "testhooks": {"ZRC4_TEST_HOOKS": 1}}      # fault injection (zrc4_ks.inc), never the product
+                 "testhooks": {"ZRC4_TEST_HOOKS": 1},      # fault injection (zrc4_ks.inc), never the product
+                 "preclaim1": {"ZRC4_GR_PRECLAIM_MAX": 1}}  # grouped claims in the loop from the 2nd bucket on
 
 
 def build_all(force: bool = False) -> None:

@@ -1731,6 +1731,13 @@ __device__ __forceinline__ BucketView bucket_read_pair(const uint32_t *grp, cons
 #ifndef ZRC4_GR_CLAIM_AB
 #define ZRC4_GR_CLAIM_AB 0       // timing-only claim forms (1: atomic without return, 2: plain store)
 #endif
+#ifndef ZRC4_GR_PRECLAIM
+#define ZRC4_GR_PRECLAIM 1       // the pair kernel claims the groups of its first buckets in the prologue
+#endif
+#ifndef ZRC4_GR_PRECLAIM_MAX
+#define ZRC4_GR_PRECLAIM_MAX 64  // how many (the lost mask is 64 bits; a test build uses 1)
+#endif
+static_assert(ZRC4_GR_PRECLAIM_MAX >= 1 && ZRC4_GR_PRECLAIM_MAX <= 64, "pre-claim mask is 64 bits");
 #ifndef ZRC4_GR_CLAIM_LAST
 #define ZRC4_GR_CLAIM_LAST 0     // the claim after the image loads (the entries' wait counts 17 younger)
 #endif
@@ -1976,6 +1983,8 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     uint32_t gcur = 0;
     bool cur_ok = false;
     uint32_t cold = 0;
+    uint64_t lostm = 0;                       // PG + ZRC4_GR_PRECLAIM: bucket k's claim lost (k < 64)
+    bool pre = false;                         // ... pre-claims on (wave-uniform)
     uint32_t qid = ZRC4_INVALID, qlen = 0;
     if constexpr (PG) {
         // Prologue (whole workgroup): bucket w's table in pair 0's region,
@@ -1988,29 +1997,134 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #pragma unroll
         for (uint32_t c = 0; c < 4u; ++c) gr[(c >> 1) * kGrPairWords + kGrPairCnt + 256u * (c & 1u) + j] = 0u;
         if (j < 4u) gr[kGrMeet + j] = 0u;
-        const uint32_t e0 = w * kGroup + j, e1 = (w + gridDim.x) * kGroup + j, e2 = e1 + gridDim.x * kGroup;
-        const uint32_t id0 = e0 < n ? ids[e0] : ZRC4_INVALID, l0 = e0 < n ? len[e0] : 0u;
-        const uint32_t id1 = e1 < n ? ids[e1] : ZRC4_INVALID, l1 = e1 < n ? len[e1] : 0u;
-        if (e2 < n) {
-            qid = ids[e2];
-            qlen = len[e2];
+        // Raw entries of this workgroup's first 8 buckets (w + k grid) in one
+        // round trip: bucket 0's table, bucket 1's staging, bucket 2's
+        // qid / qlen, and the claims below.
+        const uint32_t KB = (nwg - 1u - w) / gridDim.x + 1u;            // this workgroup's buckets (w < nwg)
+        const uint32_t K = min((uint32_t)ZRC4_GR_PRECLAIM_MAX, KB);      // ... pre-claimed
+        // Pre-claims pay two LDS rounds and a later atomic in the prologue;
+        // they win from 3 buckets per workgroup on (cfg5, 4: 293.3 -> 287.4
+        // us) and lose below (262 144 / 131 072 x 1 KiB, 2 / 1 bucket: +1.5 /
+        // +2.4 us; profiles/r04/claim3), where bucket 0 claims in the prologue
+        // and later ones in the loop, as without them.
+        pre = ZRC4_GR_PRECLAIM && KB >= 3u;
+        const uint32_t wv = __builtin_amdgcn_readfirstlane(j >> 6);
+        uint32_t idk[8], lk[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const uint32_t e = (w + m * gridDim.x) * kGroup + j;
+            const bool v = (uint32_t)m < KB && e < n;
+            idk[m] = v ? ids[e] : ZRC4_INVALID;
+            lk[m] = v ? len[e] : 0u;
         }
-        *reinterpret_cast<uint2 *>(gr + kGrStg + 512u + 2u * j) = make_uint2(id1, l1);
+        qid = idk[2];
+        qlen = lk[2];
+        *reinterpret_cast<uint2 *>(gr + kGrStg + 512u + 2u * j) = make_uint2(idk[1], lk[1]);
+#if ZRC4_GR_PRECLAIM
+        // Claims up front: each of this workgroup's first 64 buckets whose
+        // busy entries all name one group claims that group here -- one
+        // atomic per bucket and pair, all in flight together; an atomic
+        // issued at a boundary, behind the previous group's image stores,
+        // cost ~2 us of boundary each (profiles/r04/gpair4, gpair5).  A
+        // bucket naming two groups claims nothing (its table refuses it, as
+        // before); one naming a slot twice claims its group and is refused by
+        // its table (no other bucket may name that group anyway).  Bit k of
+        // lostm: bucket k's claim on part pr was already held.  Buckets from
+        // the 65th on claim in the loop.  Scratch: staging buffer 0 (first
+        // written at boundary 0) and word 12 of each pair region.
+        uint32_t *sv = gr + kGrStg;
+        auto votes = [&](const uint32_t (&ik)[8], const uint32_t (&lkk)[8]) {   // each wave's first busy group
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const uint64_t bm = __ballot(ik[m] < capacity && lkk[m] != 0u);
+                const uint32_t gs = bm ? __builtin_amdgcn_readlane(ik[m], (int)__builtin_ctzll(bm)) >> 8 : ZRC4_INVALID;
+                if ((j & 63u) == 0u) sv[4u * m + wv] = gs;
+            }
+        };
+        auto first4 = [](uint4 v) {
+            return v.x != ZRC4_INVALID ? v.x : v.y != ZRC4_INVALID ? v.y : v.z != ZRC4_INVALID ? v.z : v.w;
+        };
+        auto mixed = [&](const uint32_t (&ik)[8], const uint32_t (&lkk)[8]) {   // a busy entry of another group?
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const uint32_t g = __builtin_amdgcn_readfirstlane(first4(*reinterpret_cast<const uint4 *>(sv + 4u * m)));
+                const bool mx = __ballot(ik[m] < capacity && lkk[m] != 0u && (ik[m] >> 8) != g) != 0u;
+                if ((j & 63u) == 0u) sv[32u + 4u * m + wv] = mx ? 1u : 0u;
+            }
+        };
+        auto claim = [&](uint32_t k0) {                  // lanes 0..7 of each pair's first wave: the old words
+            const uint32_t l = j & 127u;
+            uint32_t old = 0u;
+            if (l < 8u && k0 + l < K) {
+                const uint4 mx = *reinterpret_cast<const uint4 *>(sv + 32u + 4u * l);
+                const uint32_t g = first4(*reinterpret_cast<const uint4 *>(sv + 4u * l));
+                if (g != ZRC4_INVALID && (mx.x | mx.y | mx.z | mx.w) == 0u)
+                    old = __hip_atomic_exchange(reinterpret_cast<uint32_t *>(cl.word + (size_t)g * kClaimParts + pr) + 1,
+                                                cl.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return old;
+        };
+        auto lost_to_lds = [&](uint32_t old) {           // the mask -> word 12 of the pair region
+            const uint64_t lb = __ballot(old == cl.epoch);
+            if ((j & 127u) == 0u) grp[12] = (uint32_t)lb;
+        };
+        if (pre) votes(idk, lk);
+#endif
         __syncthreads();
-        bucket_table(gr, w, id0, l0, n, capacity, err);
+        bucket_table(gr, w, idk[0], lk[0], n, capacity, err);
+#if ZRC4_GR_PRECLAIM
+        if (pre) mixed(idk, lk);
+#endif
         __syncthreads();
         const BucketView bv = bucket_read(gr, w, err);
         gcur = bv.g;
         cur_ok = bv.ok;
+#if ZRC4_GR_PRECLAIM
+        // (batch 0's answers are collected after the image loads are issued)
+        const uint32_t old0 = pre ? claim(0u) : 0u;
+        if (!pre && bv.ok && (j & 127u) == 0u)
+            cold = __hip_atomic_exchange(reinterpret_cast<uint32_t *>(cl.word + (size_t)bv.g * kClaimParts + pr) + 1,
+                                         cl.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (pre && K > 8u) {                             // (more than 4 096 buckets: 8 more per round)
+            lost_to_lds(old0);
+            __syncthreads();
+            lostm = __builtin_amdgcn_readfirstlane(grp[12]);
+            for (uint32_t k0 = 8u; k0 < K; k0 += 8u) {
+                uint32_t ik[8], lkk[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    const uint32_t e = (w + (k0 + m) * gridDim.x) * kGroup + j;
+                    const bool v = k0 + m < K && e < n;
+                    ik[m] = v ? ids[e] : ZRC4_INVALID;
+                    lkk[m] = v ? len[e] : 0u;
+                }
+                __syncthreads();                         // the previous round's scratch is read
+                votes(ik, lkk);
+                __syncthreads();
+                mixed(ik, lkk);
+                __syncthreads();
+                lost_to_lds(claim(k0));
+                __syncthreads();
+                lostm |= (uint64_t)__builtin_amdgcn_readfirstlane(grp[12]) << k0;
+            }
+        }
+#else
         if (bv.ok && (j & 127u) == 0u)
             cold = __hip_atomic_exchange(reinterpret_cast<uint32_t *>(cl.word + (size_t)bv.g * kClaimParts + (j >> 7)) + 1,
                                          cl.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         cur.len = bv.valid ? len[bv.ent] : 0u;
         cur.off = bv.valid ? off[bv.ent] : 0u;
         cur.slot = bv.valid ? bv.g * 256u + j : ZRC4_INVALID;
         cur.xy = xy[bv.g * 256u + j];
         load_image(gcur);                     // with the entry gathers, not after the barrier
+#if ZRC4_GR_PRECLAIM
+        if (pre && K <= 8u) lost_to_lds(old0);
+#endif
         __syncthreads();                      // table and votes read before the pairs build their own
+#if ZRC4_GR_PRECLAIM
+        if (pre && K <= 8u) lostm = __builtin_amdgcn_readfirstlane(grp[12]);
+#endif
     } else if constexpr (GR) {
         // Prologue: bucket w's table (compiler loads, waited for once below),
         // its claim, permuted entry, x/y and image; bucket w + grid's raw entry.
@@ -2076,7 +2190,8 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                 // from both pairs' raw entries (staging (bk + 1) & 1) once the
                 // other pair has finished boundary bk - 1, then bucket
                 // w + 2 grid's raw entries published (staging bk & 1)
-                if ((j & 127u) == 0u) grp[kGrLost] = cur_ok && cold == cl.epoch ? 1u : 0u;
+                const bool lostk = pre && bk < ZRC4_GR_PRECLAIM_MAX ? ((lostm >> bk) & 1u) != 0u : cold == cl.epoch;
+                if ((j & 127u) == 0u) grp[kGrLost] = cur_ok && lostk ? 1u : 0u;
                 if (w + gridDim.x < nwg)
                     (void)bucket_table_pair(grp, gr + kGrStg + 512u * ((bk + 1u) & 1u), w + gridDim.x, capacity, err,
                                             gr + kGrCnt + (pr ^ 1u), bk);
@@ -2180,8 +2295,9 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #ifndef ZRC4_GR_NOSWAP_AB
 #define ZRC4_GR_NOSWAP_AB 0      // timing-only: the claim word read, never swapped (claims off)
 #endif
+                const bool preclaimed = PG && pre && bk < ZRC4_GR_PRECLAIM_MAX;   // (bk: wn's index)
                 const uint32_t dc = __builtin_amdgcn_readfirstlane(
-                    !ZRC4_GR_NOSWAP_AB && nok && (j & (PG ? 127u : 255u)) < 64u ? 1u : 0u);
+                    !ZRC4_GR_NOSWAP_AB && !preclaimed && nok && (j & (PG ? 127u : 255u)) < 64u ? 1u : 0u);
                 prefetch_bucket(P, Q, ilo, ihi, cold, rlen, roff, rxy, qid, qlen,
                                 reinterpret_cast<const uint32_t *>(cl.word + (size_t)gn * kClaimParts + (PG ? pr : 0u)) + 1,
                                 cl.epoch,
