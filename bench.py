@@ -383,14 +383,14 @@ def kernel_name(S: int, ids: str = "range") -> str:
     groups = -(-S // 256)
     mode = {"range": 1, "grouped": 2, "scattered": 0}[ids]
     if ids == "scattered":
-        return "zrc4::crypt_stream_kernel<false, false>" if groups > cus else "zrc4::crypt_kernel<0, false>"
+        return "zrc4::crypt_stream_kernel<false, false, false>" if groups > cus else "zrc4::crypt_kernel<0, false>"
     if groups <= WIN_MAX_GROUPS:
         return f"zrc4::crypt_win_kernel<{mode}, false>"
     if 2 * groups <= cus:
         return f"zrc4::crypt_half_kernel<{mode}, false>"
     if groups <= cus:
         return f"zrc4::crypt_kernel<{mode}, false>"
-    return "zrc4::crypt_stream_kernel<true, true>" if ids == "grouped" else "zrc4::crypt_stream_kernel<true, false>"
+    return "zrc4::crypt_stream_kernel<true, true, false>" if ids == "grouped" else "zrc4::crypt_stream_kernel<true, false, false>"
 
 
 def load_traffic(workload: str):
