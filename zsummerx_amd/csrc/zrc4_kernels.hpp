@@ -1088,6 +1088,27 @@ __device__ __forceinline__ uint32_t xcd_run_map(uint32_t k, uint32_t grid)
     return k >= (grid & ~63u) ? k : (k & ~63u) | ((k & 7u) << 3) | ((k >> 3) & 7u);
 }
 
+// ZRC4_PAIR_DIRECT: whole-group range launches (crypt_kernel<kRange>) by
+// wave pairs as the persistent kernel (pair_meet, img_vo): each pair fills,
+// runs and copies out its half image without waiting for the other.
+// Measured, not kept: with one group per workgroup there is no boundary to
+// decouple, only the fill and the end (same process,
+// profiles/r04/pdirect/ab_direct.log: cfg3 25.50 vs 25.32 us with the
+// barriers, 65 536 x 1 KiB 58.44 vs 58.24, x 512 B 36.60 vs 36.32).
+#ifndef ZRC4_PAIR_DIRECT
+#define ZRC4_PAIR_DIRECT 0
+#endif
+__device__ __forceinline__ void pair_meet_d(uint32_t *ctr, uint32_t &gen)
+{
+    ++gen;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63u) == 0u) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+           2u * gen)
+        __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
 template <int MODE, bool FRAME, bool HALF>
 __device__ __forceinline__ void
 crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
@@ -1162,7 +1183,15 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     const bool valid = e < n;
     const uint32_t h = HALF ? (wg & 1u) : 0u;            // half of the group (HALF)
     const uint32_t j = h * 128u + tid;                   // group lane
-    const uint32_t vo0 = image_lane_offset(tid, HALF, h);
+    // (range whole groups by pairs: thread j's chunks sit in its pair's half rows)
+    constexpr bool PD = MODE == kRange && !HALF && ZRC4_PAIR_DIRECT;
+    const uint32_t vo0 = PD ? image_lane_offset(tid & 127u, true, tid >> 7) : image_lane_offset(tid, HALF, h);
+    uint32_t *pdc = reinterpret_cast<uint32_t *>(smem + kGroupBytes) + 4u + __builtin_amdgcn_readfirstlane(tid >> 7);
+    uint32_t pdg = 0;
+    if constexpr (PD) {
+        if (tid < 2u) reinterpret_cast<uint32_t *>(smem + kGroupBytes)[4u + tid] = 0u;
+        __syncthreads();
+    }
     const uint32_t col = col_of(j);
     volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(smem + kGroupBytes);
     uint4 img[16];
@@ -1337,7 +1366,8 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         if (pre) issue_block_asm(A, msg);
 #pragma unroll
         for (int i = 0; i < 16; ++i) *reinterpret_cast<uint4 *>(S + i * 4096 + vo0) = img[i];
-        __syncthreads();
+        if constexpr (PD) pair_meet_d(pdc, pdg);
+        else __syncthreads();
         if constexpr (MODE == kGrouped) {
             if (flag[3]) {                               // another bucket of this launch holds the group
                 if (tid == 0) latch_fault(err, kErrGroup);
@@ -1369,7 +1399,8 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     stamp(ts, 2);
 
     if (whole) {
-        __syncthreads();
+        if constexpr (PD) pair_meet_d(pdc, pdg);
+        else __syncthreads();
         uint8_t *img_out = arena + (size_t)g * kGroupBytes;
 #pragma unroll
         for (int i = 0; i < 16; ++i)
