@@ -2472,7 +2472,11 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 // Key schedule: key lengths dividing 16 keep a 16-byte pattern in 4 VGPRs,
 // 32- and 64-byte keys a 64-byte pattern in 16 VGPRs (step u adds pattern
 // byte (u+1) mod the chunk length through the SDWA source selector, no key
-// loads in the loop); other lengths fetch 16 key bytes one chunk ahead.
+// loads in the loop); other lengths up to 48 read 17-byte windows of the
+// schedule's first 64 bytes from LDS, longer ones fetch the 17 bytes of
+// each chunk one chunk ahead (dwords + byte aligns) -- both run the step
+// with the key byte taken by SDWA selector from the window's registers.
+// In: x0 = &S[i], x1 = &S[i+1], a0 = S[i], ya = &S[j + key[i]].
 // ---------------------------------------------------------------------------
 #define ZRC4_KSA_STEP_SEL(XC, XN, A, P, KN, SEL)                                                 \
     "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
@@ -2488,28 +2492,8 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     "src0_sel:DWORD src1_sel:BYTE_1\n\t"                                                         \
     "s_waitcnt lgkmcnt(1)\n\t"
 #define ZRC4_KSA_STEP(XC, XN, A, P, KN) ZRC4_KSA_STEP_SEL(XC, XN, A, P, KN, BYTE_0)
-#define ZRC4_KSA_PAIR(K1, K2)                                                                    \
-    ZRC4_KSA_STEP(x0, x1, a0, a1, K1) ZRC4_KSA_STEP(x1, x0, a1, a0, K2)
 #define ZRC4_KSA_QPAIR(K1, S1, K2, S2)                                                           \
     ZRC4_KSA_STEP_SEL(x0, x1, a0, a1, K1, S1) ZRC4_KSA_STEP_SEL(x1, x0, a1, a0, K2, S2)
-
-// 16 KSA steps.  In: x0 = &S[i], x1 = &S[i+1], a0 = S[i], ya = &S[j + key[i]].
-// kn[u] = key byte of step i+u+1 (kn[15] = first byte of the next chunk).
-__device__ __forceinline__ void ksa16_asm(uint32_t &x0, uint32_t &x1, uint32_t &a0, uint32_t &ya,
-                                          const uint32_t (&kn)[16])
-{
-    uint32_t a1, b;
-    asm volatile(
-        ZRC4_KSA_PAIR(k0, k1) ZRC4_KSA_PAIR(k2, k3) ZRC4_KSA_PAIR(k4, k5) ZRC4_KSA_PAIR(k6, k7)
-        ZRC4_KSA_PAIR(k8, k9) ZRC4_KSA_PAIR(k10, k11) ZRC4_KSA_PAIR(k12, k13) ZRC4_KSA_PAIR(k14, k15)
-        "s_waitcnt lgkmcnt(0)\n\t"
-        : [ya] "+v"(ya), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0), [a1] "=&v"(a1), [b] "=&v"(b)
-        : [k0] "v"(kn[0]), [k1] "v"(kn[1]), [k2] "v"(kn[2]), [k3] "v"(kn[3]), [k4] "v"(kn[4]),
-          [k5] "v"(kn[5]), [k6] "v"(kn[6]), [k7] "v"(kn[7]), [k8] "v"(kn[8]), [k9] "v"(kn[9]),
-          [k10] "v"(kn[10]), [k11] "v"(kn[11]), [k12] "v"(kn[12]), [k13] "v"(kn[13]),
-          [k14] "v"(kn[14]), [k15] "v"(kn[15])
-        : "memory");
-}
 
 // 16 KSA steps with the key bytes taken from a 16-byte pattern in registers
 // (key lengths 1, 2, 4, 8, 16).  Step u adds pattern byte (u+1) % 16.
@@ -2796,28 +2780,47 @@ ksa_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             }
             }
         } else {
-            // key bytes of steps 16c .. 16c+16, fetched one chunk ahead
+            // Longer keys (over 48 bytes but 64): the 17 key bytes of steps
+            // 16c .. 16c+16, fetched one chunk ahead -- as the 5 dwords
+            // covering them plus byte aligns while they do not wrap past the
+            // key's end (all but ~17 / len of the chunks), else byte by byte
+            // (r03 fetched every chunk as 17 byte loads: the KSA then ran at
+            // the rate of those loads, 2.1x the 16-byte time at 100 bytes).
             uint32_t kk = 0;
-            auto fetch = [&](uint32_t (&kb)[17]) {
+            auto fetch = [&](uint32_t (&q)[5]) {
+                if (kk + 17u <= kl) {
+                    const uintptr_t pa = (uintptr_t)(key + kk);
+                    const uint32_t *pw = reinterpret_cast<const uint32_t *>(pa & ~(uintptr_t)3);
+                    const uint32_t sh = (uint32_t)(pa & 3u);
+                    uint32_t d[5];
 #pragma unroll
-                for (int u = 0; u < 17; ++u) {
-                    kb[u] = key[kk];
-                    if (u < 16 && ++kk >= kl) kk = 0;   // key[k], k cycles mod len (:67-70)
+                    for (int m = 0; m < 5; ++m) d[m] = pw[m];       // (each holds a byte of the window)
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) q[m] = __builtin_amdgcn_alignbyte(d[m + 1], d[m], sh);
+                    q[4] = d[4] >> (8u * sh);
+                    kk += 16u;                                      // < len: no wrap here
+                } else {
+                    uint32_t b[17];
+#pragma unroll
+                    for (int u = 0; u < 17; ++u) {
+                        b[u] = key[kk];
+                        if (u < 16 && ++kk >= kl) kk = 0;           // key[k], k cycles mod len (:67-70)
+                    }
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        q[m] = b[4 * m] | (b[4 * m + 1] << 8) | (b[4 * m + 2] << 16) | (b[4 * m + 3] << 24);
+                    q[4] = b[16];
                 }
             };
-            uint32_t cur[17], nxt[17];
+            uint32_t cur[5], nxt[5];
             fetch(cur);
-            uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col], ya = col;
-            // j = 0 + key[0] before step 0 (the S[0] term is added inside the step)
-            ya = (ya & 0xFFu) | (((cur[0]) << 8) & 0xFF00u);
+            uint32_t x0 = col, x1 = (1u << 8) | col, a0 = S[col];
+            uint32_t ya = col | ((cur[0] & 0xFFu) << 8);   // j = 0 + key[0] before step 0
             for (int c = 0; c < 16; ++c) {
                 if (c < 15) fetch(nxt);
-                uint32_t kn[16];
+                ksa16_window_asm(x0, x1, a0, ya, cur);
 #pragma unroll
-                for (int u = 0; u < 16; ++u) kn[u] = cur[u + 1];
-                ksa16_asm(x0, x1, a0, ya, kn);
-#pragma unroll
-                for (int u = 0; u < 17; ++u) cur[u] = nxt[u];
+                for (int m = 0; m < 5; ++m) cur[m] = nxt[m];
             }
         }
     }
