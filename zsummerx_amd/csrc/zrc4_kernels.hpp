@@ -1759,9 +1759,6 @@ __device__ __forceinline__ BucketView bucket_read_pair(const uint32_t *grp, cons
     return bv;
 }
 
-#ifndef ZRC4_GR_CLAIM_AB
-#define ZRC4_GR_CLAIM_AB 0       // timing-only claim forms (1: atomic without return, 2: plain store)
-#endif
 #ifndef ZRC4_GR_PRECLAIM
 #define ZRC4_GR_PRECLAIM 1       // the pair kernel claims the groups of its first buckets in the prologue
 #endif
@@ -1769,9 +1766,6 @@ __device__ __forceinline__ BucketView bucket_read_pair(const uint32_t *grp, cons
 #define ZRC4_GR_PRECLAIM_MAX 64  // how many (the lost mask is 64 bits; a test build uses 1)
 #endif
 static_assert(ZRC4_GR_PRECLAIM_MAX >= 1 && ZRC4_GR_PRECLAIM_MAX <= 64, "pre-claim mask is 64 bits");
-#ifndef ZRC4_GR_CLAIM_LAST
-#define ZRC4_GR_CLAIM_LAST 0     // the claim after the image loads (the entries' wait counts 17 younger)
-#endif
 // The next bucket's claim (lane 0 of wave 0 swaps the launch epoch into the
 // high half of the group's part-0 claim word -- only the epoch decides a
 // claim -- and every other wave reads that half instead, so every wave issues
@@ -1791,24 +1785,16 @@ __device__ __forceinline__ void prefetch_bucket(u32x32 &P, u32x32 &Q, u32x32 &il
     uint32_t vo = img_vo(j);
     uint64_t sv;
     asm volatile(
-#if !ZRC4_GR_CLAIM_LAST
         "s_mov_b64 %[sv], exec\n\t"
         "s_mov_b64 exec, 1\n\t"
         "s_cmp_eq_u32 %[dc], 0\n\t"
         "s_cbranch_scc1 PB_READ_%=\n\t"
-#if ZRC4_GR_CLAIM_AB == 1
-        "global_atomic_swap %[cw], %[cv], off\n\t"      // timing-only: no return
-#elif ZRC4_GR_CLAIM_AB == 2
-        "global_store_dword %[cw], %[cv], off\n\t"      // timing-only: a plain store
-#else
         "global_atomic_swap %[cold], %[cw], %[cv], off sc0\n\t"
-#endif
         "s_branch PB_CLAIMED_%=\n\t"
         "PB_READ_%=:\n\t"
         "global_load_dword %[cold], %[cw], off\n\t"
         "PB_CLAIMED_%=:\n\t"
         "s_mov_b64 exec, %[sv]\n\t"
-#endif
         "global_load_dword %[rlen], %[alen], off\n\t"
         "global_load_dwordx2 %[roff], %[aoff], off\n\t"
         "global_load_ushort %[rxy], %[axy], off\n\t"
@@ -1845,24 +1831,6 @@ __device__ __forceinline__ void prefetch_bucket(u32x32 &P, u32x32 &Q, u32x32 &il
         "global_load_dwordx4 v[216:219], %[vo], %[ib]\n\t"
         "v_add_u32 %[vo], 0x1000, %[vo]\n\t"
         "global_load_dwordx4 v[220:223], %[vo], %[ib]\n\t"
-#if ZRC4_GR_CLAIM_LAST
-        "s_mov_b64 %[sv], exec\n\t"
-        "s_mov_b64 exec, 1\n\t"
-        "s_cmp_eq_u32 %[dc], 0\n\t"
-        "s_cbranch_scc1 PB_READ_%=\n\t"
-#if ZRC4_GR_CLAIM_AB == 1
-        "global_atomic_swap %[cw], %[cv], off\n\t"      // timing-only: no return
-#elif ZRC4_GR_CLAIM_AB == 2
-        "global_store_dword %[cw], %[cv], off\n\t"      // timing-only: a plain store
-#else
-        "global_atomic_swap %[cold], %[cw], %[cv], off sc0\n\t"
-#endif
-        "s_branch PB_CLAIMED_%=\n\t"
-        "PB_READ_%=:\n\t"
-        "global_load_dword %[cold], %[cw], off\n\t"
-        "PB_CLAIMED_%=:\n\t"
-        "s_mov_b64 exec, %[sv]\n\t"
-#endif
         : "+{v[40:71]}"(P), "+{v[72:103]}"(Q), "=&{v[160:191]}"(ilo), "=&{v[192:223]}"(ihi), [cold] "=&v"(cold),
           [rlen] "=&v"(rlen), [roff] "=&v"(roff), [rxy] "=&v"(rxy), [qid] "=&v"(qid), [qlen] "=&v"(qlen),
           [vo] "+v"(vo), [sv] "=&s"(sv)
@@ -2377,14 +2345,8 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                 // would also wait for it)
                 if constexpr (GR) {
                     if (!p_async) {
-#if ZRC4_GR_CLAIM_LAST
-                        // (the claim, younger than the image, is retired by the next fill's vmcnt(24))
-                        asm volatile("s_waitcnt vmcnt(17)"
-                                     : "+v"(rlen), "+v"(roff), "+v"(rxy), "+v"(cold), "+v"(qid), "+v"(qlen) :: "memory");
-#else
                         asm volatile("s_waitcnt vmcnt(16)"
                                      : "+v"(rlen), "+v"(roff), "+v"(rxy), "+v"(cold), "+v"(qid), "+v"(qlen) :: "memory");
-#endif
                     }
                     nxt.len = rlen;           // 0 for lanes without an entry (and for idle / refused buckets)
                     nxt.off = roff;
