@@ -130,24 +130,33 @@ class GpuRunner:
             # ids, as an engine's free list hands them out).  grouped: entries
             # bucketed by group -> zrc4_crypt_grouped (coalesced images);
             # scattered: the same ids unbucketed -> zrc4_crypt (per-lane gathers).
+            # (whole groups only: a short group placed mid-batch would make
+            # later buckets straddle two groups)
+            if S % 256:
+                raise SystemExit(f"--ids {ids_mode} needs a multiple of 256 sessions per batch, not {S}")
             rng = np.random.default_rng(77)
             perm = np.empty(n, dtype=np.int64)
+            bgroups = []
             for b in range(R):
-                G = -(-S // 256)
-                order = rng.permutation(G)
-                pos = 0
-                for g in order:
-                    lo, hi = b * S + g * 256, min(b * S + (g + 1) * 256, (b + 1) * S)
-                    perm[b * S + pos: b * S + pos + (hi - lo)] = lo + rng.permutation(hi - lo)
-                    pos += hi - lo
+                order = rng.permutation(S // 256)
+                bgroups.append(np.ascontiguousarray((b * S // 256 + order).astype(np.uint32)))
+                for k, g in enumerate(order):
+                    lo = b * S + g * 256
+                    perm[b * S + 256 * k: b * S + 256 * (k + 1)] = lo + rng.permutation(256)
             # entry e of batch b -> session perm[e]: keys/state/payload follow the session
             self.ids = T(perm.astype(np.int32))
             self.off = T((perm * L).astype(np.int64))
-            self._fn = lib.zrc4_crypt_grouped if ids_mode == "grouped" else lib.zrc4_crypt
+            self._bgroups = bgroups          # declared: each bucket's group (host memory)
             for b in range(R):
-                self._args.append((h, C.c_void_p(self.ids.data_ptr() + 4 * b * S), C.c_void_p(self.payload.data_ptr()),
-                                   C.c_void_p(self.off.data_ptr() + 8 * b * S),
-                                   C.c_void_p(self.len.data_ptr() + 4 * b * S), S, st))
+                common = (C.c_void_p(self.payload.data_ptr()), C.c_void_p(self.off.data_ptr() + 8 * b * S),
+                          C.c_void_p(self.len.data_ptr() + 4 * b * S), S)
+                idp = C.c_void_p(self.ids.data_ptr() + 4 * b * S)
+                if ids_mode == "declared":
+                    self._fn = lib.zrc4_crypt_grouped_declared
+                    self._args.append((h, idp, C.c_void_p(bgroups[b].ctypes.data), *common, None, st))
+                else:
+                    self._fn = lib.zrc4_crypt_grouped if ids_mode == "grouped" else lib.zrc4_crypt
+                    self._args.append((h, idp, *common, st))
 
     def step(self, i: int) -> None:
         rc = self._fn(*self._args[i % self.R])
@@ -381,16 +390,17 @@ def kernel_name(S: int, ids: str = "range") -> str:
     except Exception:
         cus = 256
     groups = -(-S // 256)
-    mode = {"range": 1, "grouped": 2, "scattered": 0}[ids]
+    mode = {"range": 1, "grouped": 2, "declared": 2, "scattered": 0}[ids]
     if ids == "scattered":
         return "zrc4::crypt_stream_kernel<false, false, false>" if groups > cus else "zrc4::crypt_kernel<0, false>"
     if groups <= WIN_MAX_GROUPS:
-        return f"zrc4::crypt_win_kernel<{mode}, false>"
+        return f"zrc4::crypt_win_kernel<{mode}, false, {'true' if ids == 'declared' else 'false'}>"
     if 2 * groups <= cus:
         return f"zrc4::crypt_half_kernel<{mode}, false>"
     if groups <= cus:
         return f"zrc4::crypt_kernel<{mode}, false>"
-    return "zrc4::crypt_stream_kernel<true, true, false>" if ids == "grouped" else "zrc4::crypt_stream_kernel<true, false, false>"
+    return ("zrc4::crypt_stream_kernel<true, true, false>" if ids in ("grouped", "declared")
+            else "zrc4::crypt_stream_kernel<true, false, false>")
 
 
 def load_traffic(workload: str):
@@ -778,9 +788,10 @@ def parse(argv=None):
                    help="CPU baseline time budget on rank 0 at N=1 (0 disables)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="cap on CPU-baseline threads (0 = every core in the affinity mask)")
-    p.add_argument("--ids", choices=["range", "grouped", "scattered"], default="range",
+    p.add_argument("--ids", choices=["range", "grouped", "declared", "scattered"], default="range",
                    help="slot addressing: contiguous range (zrc4_crypt_range), scattered slots bucketed by group "
-                        "(zrc4_crypt_grouped, the engine's path) or the same ids unbucketed (zrc4_crypt)")
+                        "(zrc4_crypt_grouped), the same with each bucket's group declared from the host "
+                        "(zrc4_crypt_grouped_declared, the engine's path) or the same ids unbucketed (zrc4_crypt)")
     p.add_argument("--event-every", type=int, default=16,
                    help="launches per HIP-event segment (kernel duration = segment time / N)")
     p.add_argument("--host-inclusive", action="store_true",

@@ -118,11 +118,19 @@ int zrc4_crypt_range(zrc4_ctx *ctx, uint32_t first_slot, uint8_t *payload,
  * touched; every other bucket runs):
  *   - a bucket whose busy entries span two groups, or name a slot twice;
  *   - a bucket naming a group another bucket of the same call holds: every
- *     bucket claims (the part of) its group it moves, and the first claimant
- *     runs.  With more buckets than CUs each bucket is checked before it
- *     claims; with fewer, the claim is taken on the bucket's first busy id
- *     while the check runs, so a bucket that breaks the one-group rule may
- *     also block the valid bucket of the group its first id names.
+ *     workgroup claims the PART of its bucket's group it moves (a dword
+ *     column on the window kernel, <= 32 buckets; a half on the half-group
+ *     and persistent kernels; the whole group otherwise), and the first
+ *     claimant of a part runs.  Claims and refusals therefore apply per part:
+ *     two buckets naming one group may each run some parts of it (each slot
+ *     is still all or nothing: crypted with its state advanced, or untouched).
+ *     A claim may be taken before the bucket's own check completes: on the
+ *     kernels with at most one bucket per CU it is taken on the bucket's
+ *     first busy id while the check runs, and on the persistent kernel
+ *     (more buckets than CUs) a bucket that names one slot twice claims its
+ *     group before its slot table refuses it.  So a bucket that breaks the
+ *     one-group or once-per-slot rule may also block a valid bucket of a
+ *     group it names.
  * An id >= capacity other than ZRC4_IDLE_SLOT is skipped and reported as
  * ZRC4_ERR_SLOT_RANGE (the rest of its bucket runs).  The claims carry a
  * per-call tag chosen on the host: a grouped call must not be captured into
@@ -132,6 +140,31 @@ int zrc4_crypt_range(zrc4_ctx *ctx, uint32_t first_slot, uint8_t *payload,
 int zrc4_crypt_grouped(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payload,
                        const uint64_t *off, const uint32_t *len, uint32_t n,
                        void *stream);
+
+/* zrc4_crypt_grouped with each bucket's group declared by the caller, who
+ * built the buckets on the host and so already knows them (the session
+ * engine, zrc4_crypt_host).  bucket_group is HOST memory of ceil(n / 256)
+ * entries, read during the call: bucket b's group (slot / 256 of its busy
+ * entries), or ZRC4_IDLE_SLOT for a bucket with no busy entry.  A group
+ * >= capacity / 256 returns ZRC4_ERR_INVALID_ARG and launches nothing.
+ * Semantics are zrc4_crypt_grouped's, plus one refusal: a bucket with a busy
+ * entry outside its declared group is refused (ZRC4_ERR_GROUP, nothing of it
+ * written).  Why: with at most 32 buckets (the 16-lanes-per-stream kernel,
+ * where the launch is one keystream chain long) the groups travel in the
+ * kernel arguments, so each bucket's state image is loaded at kernel entry
+ * instead of after a dependent read of the bucket's ids.  With more buckets
+ * the declared groups are checked by a short kernel on the same stream just
+ * before the crypt launch; a disagreeing bucket's own ids then also block
+ * the groups they name, so another bucket naming one of those groups is
+ * refused too (the rule for two buckets naming one group).  frame: NULL for
+ * no framing, else zrc4_crypt_grouped_frame's framing (below).  Device
+ * pointers apart from bucket_group; asynchronous. */
+struct zrc4_frame_args;
+int zrc4_crypt_grouped_declared(zrc4_ctx *ctx, const uint32_t *ids,
+                                const uint32_t *bucket_group, uint8_t *payload,
+                                const uint64_t *off, const uint32_t *len,
+                                uint32_t n, const struct zrc4_frame_args *frame,
+                                void *stream);
 
 /* Host-pointer variants: copy to the device (pinned staging), run, copy back,
  * block until done.  payload_bytes bounds the host payload buffer.
@@ -258,6 +291,12 @@ int zrc4_get_state(zrc4_ctx *ctx, uint32_t id, uint8_t sbox[256], uint8_t *x,
                    uint8_t *y);
 int zrc4_set_state(zrc4_ctx *ctx, uint32_t id, const uint8_t sbox[256],
                    uint8_t x, uint8_t y);
+/* Bulk export of slots [first_slot, first_slot + n): sbox[256 i .. 256 i +
+ * 255], x[i], y[i] for slot first_slot + i (host memory; blocks).  One copy of
+ * the groups' images instead of a strided copy per slot (checkpointing the
+ * sessions of a shard, the parity tests' state checks). */
+int zrc4_get_states(zrc4_ctx *ctx, uint32_t first_slot, uint32_t n,
+                    uint8_t *sbox, uint8_t *x, uint8_t *y);
 
 const char *zrc4_strerror(int code);
 const char *zrc4_version(void);

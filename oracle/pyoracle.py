@@ -244,6 +244,12 @@ class Batch:
         lib().oracle_state_to_bytes(C.byref(self.st[i]), sb, C.byref(x), C.byref(y))
         return bytes(sb), x.value, y.value
 
+    def states(self):
+        """Every stream's (box uint8[n, 256], x uint8[n], y uint8[n]) at once
+        (the int fields narrowed to bytes, as oracle_state_to_bytes does)."""
+        a = np.frombuffer(self.st, dtype=np.int32).reshape(-1, 258)[: self.n]
+        return a[:, 2:].astype(np.uint8), a[:, 0].astype(np.uint8), a[:, 1].astype(np.uint8)
+
 
 def now() -> float:
     return lib().oracle_now()

@@ -101,6 +101,32 @@ int zrc4_crypt_grouped_frame(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload,
     oracle_frame_scan(payload, f->off, f->len, f->bound, n, f->max_packets, f->npk, f->used, f->status, f->pkt_len);
     return rc;
 }
+// zrc4_crypt_grouped_declared: a bucket with a busy entry outside its
+// declared group is skipped (ZRC4_ERR_GROUP), then zrc4_crypt_grouped.
+int zrc4_crypt_grouped_declared(zrc4_ctx *c, const uint32_t *ids, const uint32_t *bg, uint8_t *payload,
+                                const uint64_t *off, const uint32_t *len, uint32_t n,
+                                const struct zrc4_frame_args *f, void *s)
+{
+    if (n && (!ids || !bg)) return ZRC4_ERR_INVALID_ARG;
+    const uint32_t groups = (uint32_t)((c->st.size() + 255) / 256);
+    for (uint32_t b = 0; b < (n + 255) / 256; ++b)
+        if (bg[b] >= groups && bg[b] != ZRC4_IDLE_SLOT) return ZRC4_ERR_INVALID_ARG;
+    std::vector<uint32_t> kept(ids, ids + n);
+    int rc = ZRC4_OK;
+    for (uint32_t b = 0; b < n; b += 256) {
+        const uint32_t e = b + 256 < n ? b + 256 : n;
+        bool bad = false;
+        for (uint32_t i = b; i < e; ++i)
+            if (len[i] && ids[i] != ZRC4_IDLE_SLOT && ids[i] < c->st.size() && ids[i] / 256 != bg[b / 256]) bad = true;
+        if (bad) {
+            rc = ZRC4_ERR_GROUP;
+            for (uint32_t i = b; i < e; ++i) kept[i] = ZRC4_IDLE_SLOT;
+        }
+    }
+    const int r2 = f ? zrc4_crypt_grouped_frame(c, kept.data(), payload, off, len, n, f, s)
+                     : zrc4_crypt_grouped(c, kept.data(), payload, off, len, n, s);
+    return r2 ? r2 : rc;
+}
 int zrc4_xor_ring(zrc4_ctx *, uint8_t *ring, uint32_t cap, const uint32_t *rid, const uint32_t *pos,
                   uint8_t *payload, const uint64_t *off, const uint32_t *len, uint32_t n, void *)
 {

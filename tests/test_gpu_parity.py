@@ -621,7 +621,7 @@ def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb, variant
     bucket's group a group ahead; from 3 buckets per workgroup (1600) the
     first 64 of a workgroup in its prologue instead -- the preclaim1 test
     build pre-claims only the first, so the contested buckets meet across
-    both paths).  At 1600 buckets every 5th uncontested entry is checked."""
+    both paths).  Every entry is checked (states read back in one copy)."""
     torch = torch_cuda
     from zsummerx_amd._capi import IDLE_SLOT
     rng = np.random.default_rng(500 + nb)
@@ -661,18 +661,17 @@ def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb, variant
             c.sync(s)
         assert ei.value.code == -7                      # ZRC4_ERR_GROUP
         got = pay.cpu().numpy()
+        gsb, gx, gy = c.get_states(0, cap)             # every device state in one copy
         crypted = untouched = 0
         for e in np.flatnonzero(busy):
             slot, a, z = int(ids[e]), int(off[e]), int(off[e] + L[e])
-            if nb > 1000 and slot // 256 != contested and e % 5:
-                continue
             before = ob.state(slot)
             want = data[a:z].copy()
             st = ob.st[slot]
             saved = pyoracle.C.create_string_buffer(bytes(st), pyoracle.C.sizeof(st))
             pyoracle.lib().oracle_encryption(pyoracle.C.byref(st), pyoracle.C.c_void_p(want.ctypes.data), int(L[e]))
             after = ob.state(slot)
-            sb, x, y = c.get_state(slot)
+            sb, x, y = gsb[slot].tobytes(), int(gx[slot]), int(gy[slot])
             if slot // 256 != contested:
                 assert np.array_equal(got[a:z], want), (e, slot)
                 assert (sb, x, y) == (bytes(after[0]), after[1], after[2]), slot
@@ -776,35 +775,58 @@ def test_grouped_stream_refusals(built, torch_cuda, variant):
 
 
 # ------------------------------------------------ full BASELINE-size configs
-def _device_workload(ctx, w, torch):
+def _device_workload(ctx, w, torch, ids_mode="range"):
+    """Seed, pre-advance and crypt the synthetic workload once.  range: entry
+    i = slot i (zrc4_crypt, identity ids); grouped / declared: the engine's
+    shape -- groups in random order, slots permuted inside each group, entry
+    e crypting session perm[e]'s payload (zrc4_crypt_grouped /
+    zrc4_crypt_grouped_declared).  Every session is crypted once either way,
+    so the ciphertext and the states are the same."""
     dev = "cuda"
-    t = lambda a: torch.from_numpy(a.view(np.uint8) if a.dtype == np.uint8 else a).to(dev)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     s = torch.cuda.current_stream()
     ctx.ksa(t(w.key_len.view(np.int32)), t(w.key_off.view(np.int64)), t(w.keys), stream=s)
     scratch = torch.zeros(1000, dtype=torch.uint8, device=dev)
     zero = torch.zeros(w.n, dtype=torch.int64, device=dev)
     ctx.crypt(scratch, zero, t(w.adv.view(np.int32)), stream=s)   # pre-advance
     pay = t(w.payload)
-    ctx.crypt(pay, t(w.off.view(np.int64)), t(w.length.view(np.int32)), stream=s)
+    if ids_mode == "range":
+        ctx.crypt(pay, t(w.off.view(np.int64)), t(w.length.view(np.int32)), stream=s)
+    else:
+        assert w.n % 256 == 0
+        rng = np.random.default_rng(2024)
+        order = rng.permutation(w.n // 256)
+        perm = (order[:, None] * 256 + np.stack([rng.permutation(256) for _ in order])).reshape(-1)
+        ids, off, ln = t(perm.astype(np.uint32).view(np.int32)), t(w.off[perm].view(np.int64)), \
+            t(w.length[perm].view(np.int32))
+        if ids_mode == "grouped":
+            ctx.crypt_grouped(pay, off, ln, ids, stream=s)
+        else:
+            ctx.crypt_grouped_declared(pay, off, ln, ids, order.astype(np.uint32), stream=s)
     ctx.sync(s)
     return pay.cpu().numpy()
 
 
 def _states_digest(ctx, n):
-    h = hashlib.sha256()
-    for i in range(n):
-        sb, x, y = ctx.get_state(i)
-        h.update(sb + bytes([x, y]))
-    return h.hexdigest()
+    """sha256 over slots 0..n-1 of sbox + x + y (zrc4_get_states: one copy)."""
+    sb, x, y = ctx.get_states(0, n)
+    return hashlib.sha256(np.concatenate([sb, x[:, None], y[:, None]], axis=1).tobytes()).hexdigest()
 
 
-@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4", "cfg5"])
-def test_baseline_configs_bit_exact(cfg, synth_digests, torch_cuda, built):
+@pytest.mark.parametrize("cfg,ids_mode", [("cfg2", "range"), ("cfg3", "range"), ("cfg4", "range"),
+                                          ("cfg5", "range"), ("cfg2", "grouped"), ("cfg2", "declared"),
+                                          ("cfg3", "declared"), ("cfg5", "grouped"), ("cfg5", "declared")])
+def test_baseline_configs_bit_exact(cfg, ids_mode, synth_digests, torch_cuda, built):
+    """BASELINE configs[1..4] at full size against SHA-256 digests made by the
+    real reference header (tests/golden/make_golden.py): the range path, and
+    the engine's grouped paths (zrc4_crypt_grouped, and _declared: the window
+    kernel with declared groups at cfg2, the declared check + persistent
+    kernel at cfg3 / cfg5)."""
     S, L = synth.CONFIGS[cfg]
     d = synth_digests[cfg]
     w = synth.make(0, S, L, threads=8)
     with Context(0, S) as c:
-        out = _device_workload(c, w, torch_cuda)
+        out = _device_workload(c, w, torch_cuda, ids_mode)
         assert hashlib.sha256(out.tobytes()).hexdigest() == d["ciphertext_sha256"], cfg
         if S <= 65536:
             assert _states_digest(c, S) == d["states_sha256"], cfg

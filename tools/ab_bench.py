@@ -52,9 +52,11 @@ def main():
     ap.add_argument("--segment", action="store_true",
                     help="time each round's launches as one back-to-back segment (per-launch average)")
     ap.add_argument("--no-check", action="store_true", help="timing-only ablation builds (outputs differ)")
-    ap.add_argument("--ids", choices=["range", "grouped"], default="range",
-                    help="grouped: zrc4_crypt_grouped over the same batches with slots permuted inside each "
-                         "group and groups in random order (bench.py --ids grouped)")
+    ap.add_argument("--ids", default="range",
+                    help="comma list of range | grouped | declared; grouped: zrc4_crypt_grouped over the same "
+                         "batches with slots permuted inside each group and groups in random order (bench.py "
+                         "--ids grouped); declared: the same through zrc4_crypt_grouped_declared.  Every "
+                         "variant runs every mode (its own context each), interleaved")
     args = ap.parse_args()
 
     from zsummerx_amd import build
@@ -70,7 +72,13 @@ def main():
     import torch  # one HIP runtime for every variant library (see _capi.load)
     from zsummerx_amd import _capi, synth
 
-    libs = [(n, _capi.load(p)) for n, p in variants]
+    modes = args.ids.split(",")
+    for m in modes:
+        if m not in ("range", "grouped", "declared"):
+            raise SystemExit(f"--ids: unknown mode {m}")
+    loaded = [(n, _capi.load(p)) for n, p in variants]
+    # one run per (variant, mode); names carry the mode when several are compared
+    libs = [((n if len(modes) == 1 else f"{n}/{m}"), lib, m) for n, lib in loaded for m in modes]
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
     st = C.c_void_p(stream.cuda_stream)
@@ -96,32 +104,36 @@ def main():
         ln = torch.full((n,), L, dtype=torch.int32, device=dev)
         scratch = torch.zeros(1000, dtype=torch.uint8, device=dev)
         zoff = torch.zeros(n, dtype=torch.int64, device=dev)
-        gids = None
-        if args.ids == "grouped":
-            # entry e of batch b -> session perm[e] (its slot, key, state and payload)
+        gids = goff = None
+        bgroups = []
+        if any(m != "range" for m in modes):
+            # entry e of batch b -> session perm[e] (its slot, key, state and
+            # payload); whole groups only (a short group mid-batch would make
+            # later buckets straddle two groups)
+            if S % 256:
+                raise SystemExit(f"{wl}: grouped modes need a multiple of 256 sessions")
             rng = np.random.default_rng(77)
             perm = np.empty(n, dtype=np.int64)
             for b in range(R):
-                Gs = -(-S // 256)
-                pos = 0
-                for g in rng.permutation(Gs):
-                    lo, hi = b * S + g * 256, min(b * S + (g + 1) * 256, (b + 1) * S)
-                    perm[b * S + pos: b * S + pos + (hi - lo)] = lo + rng.permutation(hi - lo)
-                    pos += hi - lo
+                order = rng.permutation(S // 256)
+                bgroups.append(np.ascontiguousarray((b * S // 256 + order).astype(np.uint32)))
+                for k, g in enumerate(order):
+                    perm[b * S + 256 * k: b * S + 256 * (k + 1)] = b * S + g * 256 + rng.permutation(256)
             gids = torch.from_numpy(perm.astype(np.int32)).to(dev)
-            off = torch.from_numpy(perm * L).to(dev)
+            goff = torch.from_numpy(perm * L).to(dev)
 
-        def crypt(lib, h, b, buf=None):
-            if gids is None:
-                return lib.zrc4_crypt_range(h, b * S, C.c_void_p((pay if buf is None else buf).data_ptr()),
-                                            C.c_void_p(off.data_ptr() + 8 * b * S),
-                                            C.c_void_p(ln.data_ptr() + 4 * b * S), S, st)
-            return lib.zrc4_crypt_grouped(h, C.c_void_p(gids.data_ptr() + 4 * b * S),
-                                          C.c_void_p((pay if buf is None else buf).data_ptr()),
-                                          C.c_void_p(off.data_ptr() + 8 * b * S),
-                                          C.c_void_p(ln.data_ptr() + 4 * b * S), S, st)
+        def crypt(lib, mode, h, b, buf=None):
+            p = C.c_void_p((pay if buf is None else buf).data_ptr())
+            lp = C.c_void_p(ln.data_ptr() + 4 * b * S)
+            if mode == "range":
+                return lib.zrc4_crypt_range(h, b * S, p, C.c_void_p(off.data_ptr() + 8 * b * S), lp, S, st)
+            ip, op = C.c_void_p(gids.data_ptr() + 4 * b * S), C.c_void_p(goff.data_ptr() + 8 * b * S)
+            if mode == "declared":
+                return lib.zrc4_crypt_grouped_declared(h, ip, C.c_void_p(bgroups[b].ctypes.data), p, op, lp, S,
+                                                       None, st)
+            return lib.zrc4_crypt_grouped(h, ip, p, op, lp, S, st)
         ctxs = []
-        for name, lib in libs:
+        for name, lib, _ in libs:
             h = C.c_void_p()
             _capi.check(lib.zrc4_create(C.byref(h), 0, n), f"{name} create")
             _capi.check(lib.zrc4_ksa_range(h, 0, C.c_void_p(keys.data_ptr()), C.c_void_p(koff.data_ptr()),
@@ -132,9 +144,9 @@ def main():
         torch.cuda.synchronize()
         # identical-output check on batch 0
         ref = None
-        for (name, lib), h in zip(libs, ctxs):
+        for (name, lib, mode), h in zip(libs, ctxs):
             buf = pay[: S * L].clone()
-            _capi.check(crypt(lib, h, 0, buf))
+            _capi.check(crypt(lib, mode, h, 0, buf))
             _capi.check(lib.zrc4_sync(h, st))
             if ref is None:
                 ref = buf
@@ -142,9 +154,9 @@ def main():
                 raise SystemExit(f"variant {name} output differs from {libs[0][0]} on {wl}")
         if args.ksa:
             # connection-storm KSA timing: the batch-0 sessions re-seeded per launch
-            kt = {name: [] for name, _ in libs}
+            kt = {name: [] for name, _, _ in libs}
             for r in range(args.rounds):
-                for (name, lib), h in zip(libs, ctxs):
+                for (name, lib, _), h in zip(libs, ctxs):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
                     for i in range(args.launches):
@@ -157,10 +169,10 @@ def main():
                                           "streams_per_s": round(S / (statistics.median(t) * 1e-6), 1)}
                                    for name, t in kt.items()}
             print(wl + "_ksa", json.dumps(report[wl + "_ksa"]), flush=True)
-        times = {name: [] for name, _ in libs}
+        times = {name: [] for name, _, _ in libs}
         step = 1
         for r in range(args.rounds):
-            for (name, lib), h in zip(libs, ctxs):
+            for (name, lib, mode), h in zip(libs, ctxs):
                 evs = []
                 if args.segment:               # back-to-back launches, like bench.py (kernel boundaries included)
                     s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -171,7 +183,7 @@ def main():
                     if not args.segment:
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record(stream)
-                    rc = crypt(lib, h, b)
+                    rc = crypt(lib, mode, h, b)
                     if not args.segment:
                         e1.record(stream)
                         evs.append((e0, e1))
@@ -189,9 +201,9 @@ def main():
                              "hbm_frac": round(B / (statistics.median(t) * 1e-6) / 8e12, 4)}
                       for name, t in times.items()}
         print(wl, json.dumps(report[wl]), flush=True)
-        for (name, lib), h in zip(libs, ctxs):
+        for (name, lib, _), h in zip(libs, ctxs):
             lib.zrc4_destroy(h)
-        del keys, adv, pay, off, ln, klen, koff, zoff, gids
+        del keys, adv, pay, off, ln, klen, koff, zoff, gids, goff
         torch.cuda.empty_cache()
     print(json.dumps(report))
 

@@ -74,6 +74,7 @@ class Insn:
     regs: frozenset = field(default_factory=frozenset)
 
 
+
 def _unbundle(lib: Path, td: str) -> Path:
     fb, co = Path(td) / "fb.bin", Path(td) / "co.o"
     subprocess.run([str(LLVM / "llvm-objcopy"), f"--dump-section=.hip_fatbin={fb}", str(lib), str(Path(td) / "x")],
@@ -714,7 +715,8 @@ def bool_step(ins: Insn, bc: dict, cond) -> dict:
     return bc
 
 
-def check_function(name: str, insns: list[Insn], max_states: int = 400000, debug: dict | None = None):
+def check_function(name: str, insns: list[Insn], max_states: int = 400000, debug: dict | None = None,
+                   track_partial: bool = False):
     if not insns:
         return [], 0
     idx = {i.addr: k for k, i in enumerate(insns)}
@@ -752,11 +754,15 @@ def check_function(name: str, insns: list[Insn], max_states: int = 400000, debug
     #     have in flight).
     #   full: EXEC holds every lane of the wave (all launches use whole waves).
     #   sg: SGPR operands known to hold the full mask (saved EXEC).
-    # Only loads issued with the full EXEC are tracked: the counted-wait
-    # discipline of the hand-written loops issues every VMEM op under the
-    # full mask, and a per-lane (partial-EXEC) load is followed by code whose
-    # lanes the analysis cannot tell apart.  Any access to such a register by
-    # any lane before the covering wait is a hazard.
+    # Loads issued with the full EXEC are tracked; with track_partial, every
+    # load is, whatever EXEC held: a load under a partial mask (the grouped
+    # claim, issued by lane 0 alone) writes its lanes of the destination when
+    # it returns, so a copy or move of that register by the compiler before
+    # the covering wait would read a stale value in those lanes.  Any access
+    # to a tracked register by any lane before the covering wait is a hazard
+    # (conservative for the other lanes).  Partial tracking multiplies the
+    # pending sets of compiler code with many per-lane loads, so it is asked
+    # for on the persistent kernels, where the asm-issued claim lives.
     def merge(x, y, widen):
         px, fx, sx, ix, bx = x
         py, fy, sy, iy, by = y
@@ -841,7 +847,7 @@ def check_function(name: str, insns: list[Insn], max_states: int = 400000, debug
                 if bad:
                     hazards.setdefault(ins.addr, (ins, sorted(bad), next(first_load[d] for d in st if d & bad)))
                 st = {d: y + 1 for d, y in st.items() if y + 1 < VMCNT_MAX}
-                if dest and full:
+                if dest and (full or track_partial):
                     first_load.setdefault(dest, ins.addr)
                     st[dest] = 0
                 if dest and debug is not None:

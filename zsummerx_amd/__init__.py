@@ -131,6 +131,20 @@ class Context:
         check(self._lib.zrc4_crypt_grouped(self._h, _ptr(ids), _ptr(payload), _ptr(off), _ptr(length),
                                            n, _stream(stream)), "zrc4_crypt_grouped")
 
+    def crypt_grouped_declared(self, payload, off, length, ids, bucket_group, frame: dict | None = None, n=None,
+                               stream=None) -> None:
+        """zrc4_crypt_grouped_declared: zrc4_crypt_grouped with each bucket's
+        group given from the host (bucket_group: ceil(n/256) ints, IDLE_SLOT
+        for an idle bucket); optional framing as crypt_grouped_frame."""
+        n = int(length.numel() if n is None else n)
+        bg = np.ascontiguousarray(bucket_group, dtype=np.uint32)
+        if bg.size < -(-n // GROUP_SLOTS):
+            raise ValueError("bucket_group needs one entry per 256-entry bucket")
+        fa = self._frame(frame) if frame is not None else None
+        check(self._lib.zrc4_crypt_grouped_declared(self._h, _ptr(ids), _ptr(bg), _ptr(payload), _ptr(off),
+                                                    _ptr(length), n, C.byref(fa) if fa is not None else None,
+                                                    _stream(stream)), "zrc4_crypt_grouped_declared")
+
     @staticmethod
     def _frame(frame: dict) -> FrameArgs:
         return FrameArgs(_ptr(frame["off"]), _ptr(frame["len"]), int(frame["bound"]), int(frame.get("max_packets", 0)),
@@ -217,6 +231,16 @@ class Context:
         check(self._lib.zrc4_get_state(self._h, int(slot), sbox, C.byref(x), C.byref(y)),
               "zrc4_get_state")
         return bytes(sbox), x.value, y.value
+
+    def get_states(self, first_slot: int, n: int):
+        """zrc4_get_states: (sbox uint8[n, 256], x uint8[n], y uint8[n]) of
+        slots first_slot .. first_slot + n - 1 in one copy."""
+        sb = np.empty((n, 256), dtype=np.uint8)
+        x = np.empty(n, dtype=np.uint8)
+        y = np.empty(n, dtype=np.uint8)
+        check(self._lib.zrc4_get_states(self._h, int(first_slot), int(n), _ptr(sb), _ptr(x), _ptr(y)),
+              "zrc4_get_states")
+        return sb, x, y
 
     def set_state(self, slot: int, sbox: bytes, x: int, y: int) -> None:
         if len(sbox) != 256:

@@ -42,6 +42,7 @@ SIGNATURES = [
     ("zrc4_ksa_range", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_crypt_range", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P]),
     ("zrc4_crypt_grouped", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
+    ("zrc4_crypt_grouped_declared", C.c_int, [_P, _P, _P, _P, _P, _P, C.c_uint32, _P, _P]),
     ("zrc4_crypt_range_frame", C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P]),
     ("zrc4_crypt_grouped_frame", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P, _P]),
     ("zrc4_ksa_host", C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, C.c_uint32]),
@@ -60,6 +61,7 @@ SIGNATURES = [
     ("zrc4_poll_faults", C.c_int, [_P]),
     ("zrc4_get_state", C.c_int, [_P, C.c_uint32, _U8P, _U8P, _U8P]),
     ("zrc4_set_state", C.c_int, [_P, C.c_uint32, _U8P, C.c_uint8, C.c_uint8]),
+    ("zrc4_get_states", C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P]),
     ("zrc4_strerror", C.c_char_p, [C.c_int]),
     ("zrc4_version", C.c_char_p, []),
 ]

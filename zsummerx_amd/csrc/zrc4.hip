@@ -22,6 +22,7 @@
 #define ZRC4_WIN_MAX_GROUPS 32   // aligned range and grouped batches of at most this many groups run
                                  // 16 lanes per stream (crypt_win_kernel, zrc4_win.hpp); 0 = never
 #endif
+static_assert(ZRC4_WIN_MAX_GROUPS <= zrc4::kWinMaxBuckets, "declared window groups travel in WinGroups");
 
 struct zrc4_ctx {
     int device;
@@ -43,6 +44,8 @@ struct zrc4_ctx {
     hipStream_t stream;     // private stream for the host entry points
     unsigned long long *claim;   // grouped launches' (group, part) claim words (zrc4::Claim), zeroed
     uint32_t epoch;              // the last grouped launch's claim tag
+    uint32_t *d_decl;            // declared bucket groups of a large declared launch (decl_check_kernel)
+    uint32_t d_decl_cap;         // ... its capacity in buckets
 };
 
 namespace {
@@ -90,9 +93,16 @@ constexpr size_t kZeroCopyMax = 256u << 10;   // *_host batches up to this size 
 // (cfg2 56.1 vs 48.8 us, cfg3 28.1 vs 22.7 us; profiles/r02_ab_dpp_direct.log).
 // With `fr`, the framing walk of every entry runs in the same launch: in the
 // direct kernels' epilogue, or in the persistent kernel's tail.
+//
+// `decl` (kGrouped only): the caller's declared group per 256-entry bucket, in
+// host memory (zrc4_crypt_grouped_declared).  Window launches take it in the
+// kernel arguments (the image leaves at kernel entry); larger launches check
+// it first in decl_check_kernel, which blocks the groups of a disagreeing
+// bucket through the claims.  `decl_trusted`: the groups were computed here
+// from host ids (zrc4_crypt_host), so larger launches skip the check.
 int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot, uint8_t *payload,
                  const uint64_t *off, const uint32_t *len, uint32_t n, hipStream_t s,
-                 const zrc4::FrameArgs *fr = nullptr)
+                 const zrc4::FrameArgs *fr = nullptr, const uint32_t *decl = nullptr, bool decl_trusted = false)
 {
     if (n == 0) return ZRC4_OK;
     if (mode == zrc4::kRange && (uint64_t)first_slot + n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
@@ -119,19 +129,41 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
         ((mode == zrc4::kRange && (first_slot & 255u) == 0u) || mode == zrc4::kGrouped)) {
         const dim3 wgrid(64u * grid), wblk(64);
         const zrc4::FrameArgs fa = fr ? *fr : zrc4::FrameArgs{};
+        zrc4::WinGroups dg{};
+        if (decl && mode == zrc4::kGrouped)
+            for (uint32_t b = 0; b < grid; ++b) dg.g[b] = decl[b];
+#define ZRC4_WIN(MODE_, FRAME_, DECL_)                                                                          \
+    hipLaunchKernelGGL((zrc4::crypt_win_kernel<MODE_, FRAME_, DECL_>), wgrid, wblk, 0, s, c->arena, c->xy, ids, \
+                       first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl, dg)
         if (mode == zrc4::kRange && fr)
-            hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kRange, true>), wgrid, wblk, 0, s, c->arena, c->xy, ids,
-                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl);
+            ZRC4_WIN(zrc4::kRange, true, false);
         else if (mode == zrc4::kRange)
-            hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kRange, false>), wgrid, wblk, 0, s, c->arena, c->xy, ids,
-                               first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl);
+            ZRC4_WIN(zrc4::kRange, false, false);
+        else if (decl && fr)
+            ZRC4_WIN(zrc4::kGrouped, true, true);
+        else if (decl)
+            ZRC4_WIN(zrc4::kGrouped, false, true);
         else if (fr)
-            hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kGrouped, true>), wgrid, wblk, 0, s, c->arena, c->xy,
-                               ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl);
+            ZRC4_WIN(zrc4::kGrouped, true, false);
         else
-            hipLaunchKernelGGL((zrc4::crypt_win_kernel<zrc4::kGrouped, false>), wgrid, wblk, 0, s, c->arena, c->xy,
-                               ids, first_slot, payload, off, len, n, c->capacity, c->err, c->sink, fa, cl);
+            ZRC4_WIN(zrc4::kGrouped, false, false);
+#undef ZRC4_WIN
         return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
+    }
+    if (decl && mode == zrc4::kGrouped && !decl_trusted) {
+        // check the declared groups before the crypt launch (stream-ordered):
+        // a disagreeing bucket's groups are claimed under this launch's epoch
+        if (grid > c->d_decl_cap) {
+            if (c->d_decl) (void)hipFree(c->d_decl);
+            c->d_decl = nullptr;
+            c->d_decl_cap = 0;
+            if (hipMalloc(&c->d_decl, (size_t)grid * 4u) != hipSuccess) return ZRC4_ERR_OUT_OF_MEMORY;
+            c->d_decl_cap = grid;
+        }
+        ZRC4_TRY(hipMemcpyAsync(c->d_decl, decl, (size_t)grid * 4u, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(zrc4::decl_check_kernel, dim3(grid), blk, 0, s, ids, len, n, c->d_decl, c->capacity,
+                           cl, c->err);
+        if (hipGetLastError() != hipSuccess) return ZRC4_ERR_LAUNCH;
     }
     // Few whole groups: half-group workgroups, one per CU (2 waves per CU).
     // A grouped bucket's slots may sit in either half whatever its entry
@@ -294,6 +326,7 @@ int zrc4_destroy(zrc4_ctx *c)
     if (c->xy) (void)hipFree(c->xy);
     if (c->sink) (void)hipFree(c->sink);
     if (c->claim) (void)hipFree(c->claim);
+    if (c->d_decl) (void)hipFree(c->d_decl);
     if (c->err) (void)hipHostFree(c->err);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -396,6 +429,24 @@ int zrc4_crypt_grouped_frame(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload,
     return launch_crypt(c, zrc4::kGrouped, ids, 0, payload, off, len, n, (hipStream_t)stream, &fr);
 }
 
+int zrc4_crypt_grouped_declared(zrc4_ctx *c, const uint32_t *ids, const uint32_t *bucket_group, uint8_t *payload,
+                                const uint64_t *off, const uint32_t *len, uint32_t n,
+                                const struct zrc4_frame_args *frame, void *stream)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n && (!ids || !bucket_group || !payload || !off || !len)) return ZRC4_ERR_INVALID_ARG;
+    const uint32_t nb = (uint32_t)(((uint64_t)n + zrc4::kGroup - 1) / zrc4::kGroup);
+    const uint32_t groups = c->capacity / zrc4::kGroup;
+    for (uint32_t b = 0; b < nb; ++b)
+        if (bucket_group[b] >= groups && bucket_group[b] != ZRC4_IDLE_SLOT) return ZRC4_ERR_INVALID_ARG;
+    zrc4::FrameArgs fr;
+    int rc = frame ? frame_args(frame, n, fr) : ZRC4_OK;
+    if (rc) return rc;
+    if ((rc = set_device(c))) return rc;
+    return launch_crypt(c, zrc4::kGrouped, ids, 0, payload, off, len, n, (hipStream_t)stream, frame ? &fr : nullptr,
+                        bucket_group);
+}
+
 int zrc4_xor_ring(zrc4_ctx *c, uint8_t *ring, uint32_t ring_cap, const uint32_t *rid,
                   const uint32_t *pos, uint8_t *payload, const uint64_t *off, const uint32_t *len,
                   uint32_t n, void *stream)
@@ -491,7 +542,7 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
     // coalesced image instead of 256 strided byte accesses per slot.  A slot
     // may appear once per call (as for every batched entry point).
     const bool grouped = ids && n > 1;
-    std::vector<uint32_t> order;
+    std::vector<uint32_t> order, bgroup;     // bgroup: each bucket's group, declared to the kernel
     uint32_t buckets = 0;
     if (grouped) {
         order.resize(n);
@@ -499,7 +550,10 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
         std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ids[a] < ids[b]; });
         for (uint32_t k = 0; k < n; ++k) {
             if (k && ids[order[k]] == ids[order[k - 1]]) return ZRC4_ERR_INVALID_ARG;
-            if (!k || (ids[order[k]] >> 8) != (ids[order[k - 1]] >> 8)) ++buckets;
+            if (!k || (ids[order[k]] >> 8) != (ids[order[k - 1]] >> 8)) {
+                ++buckets;
+                bgroup.push_back(ids[order[k]] >> 8);
+            }
         }
     }
     const uint32_t m = grouped ? buckets * zrc4::kGroup : n;      // entries the kernel sees
@@ -546,7 +600,8 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
     }
     rc = launch_crypt(c, grouped ? zrc4::kGrouped : ids ? zrc4::kIds : zrc4::kRange,
                       ids ? (const uint32_t *)(st + o_ids) : nullptr, 0, st + o_pay, (const uint64_t *)(st + o_off),
-                      (const uint32_t *)(st + o_len), m, c->stream);
+                      (const uint32_t *)(st + o_len), m, c->stream, nullptr, grouped ? bgroup.data() : nullptr,
+                      true);
     if (rc) return rc;
     if (payload_bytes && !zero_copy)
         ZRC4_TRY(hipMemcpyAsync(c->h_stage + o_pay, c->d_stage + o_pay, payload_bytes,
@@ -613,6 +668,37 @@ int zrc4_set_state(zrc4_ctx *c, uint32_t id, const uint8_t sbox[256], uint8_t x,
     ZRC4_TRY(hipMemcpy2DAsync(img + col, 256, tmp, 1, 1, 256, hipMemcpyHostToDevice, c->stream));
     ZRC4_TRY(hipMemcpyAsync(c->xy + id, &v, 2, hipMemcpyHostToDevice, c->stream));
     ZRC4_TRY(hipStreamSynchronize(c->stream));
+    return ZRC4_OK;
+}
+
+int zrc4_get_states(zrc4_ctx *c, uint32_t first_slot, uint32_t n, uint8_t *sbox, uint8_t *x, uint8_t *y)
+{
+    if (!c) return ZRC4_ERR_INVALID_ARG;
+    if (n == 0) return ZRC4_OK;
+    if (!sbox || !x || !y) return ZRC4_ERR_INVALID_ARG;
+    if ((uint64_t)first_slot + n > c->capacity) return ZRC4_ERR_SLOT_RANGE;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const uint32_t g0 = first_slot / zrc4::kGroup, g1 = (first_slot + n - 1) / zrc4::kGroup;
+    std::vector<uint8_t> img;
+    std::vector<uint16_t> v(n);
+    try {
+        img.resize((size_t)(g1 - g0 + 1) * zrc4::kGroupBytes);
+    } catch (const std::bad_alloc &) {
+        return ZRC4_ERR_OUT_OF_MEMORY;
+    }
+    ZRC4_TRY(hipMemcpyAsync(img.data(), c->arena + (size_t)g0 * zrc4::kGroupBytes, img.size(), hipMemcpyDeviceToHost,
+                            c->stream));
+    ZRC4_TRY(hipMemcpyAsync(v.data(), c->xy + first_slot, (size_t)n * 2u, hipMemcpyDeviceToHost, c->stream));
+    ZRC4_TRY(hipStreamSynchronize(c->stream));
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t id = first_slot + i, j = id & 255u;
+        const uint8_t *g = img.data() + (size_t)(id / zrc4::kGroup - g0) * zrc4::kGroupBytes + zrc4::col_of(j);
+        uint8_t *o = sbox + (size_t)i * 256u;
+        for (uint32_t k = 0; k < 256u; ++k) o[k] = g[k << 8];
+        x[i] = (uint8_t)(v[i] & 255u);
+        y[i] = (uint8_t)(v[i] >> 8);
+    }
     return ZRC4_OK;
 }
 

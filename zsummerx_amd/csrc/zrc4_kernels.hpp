@@ -96,7 +96,7 @@ __device__ __forceinline__ bool lds_base_ok(const uint8_t *S, uint32_t *err)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t col_of(uint32_t j)
+__host__ __device__ __forceinline__ uint32_t col_of(uint32_t j)
 {
     const uint32_t w = j >> 6, l = j & 63u;
     return ((l & 31u) << 2) | (l >> 5) | ((w & 1u) << 1) | ((w >> 1) << 7);
@@ -856,6 +856,34 @@ __device__ __forceinline__ bool crypt_message_dpp(uint8_t *S, Rc4Lane &st, uint8
 }
 
 #define ZRC4_INVALID 0xFFFFFFFFu
+
+// zrc4_crypt_grouped_declared with more buckets than the window kernel takes:
+// the caller's declared groups (decl[b], ZRC4_INVALID = an idle bucket) are
+// checked here, one workgroup per bucket, just before the crypt launch on the
+// same stream.  A bucket with a busy entry (id < capacity, len > 0) outside
+// its declared group latches kErrGroup and writes the crypt launch's epoch
+// into every claim part of each group its busy entries name: the crypt
+// kernel's workgroups that claim those groups then read back this launch's
+// epoch and store nothing (the rule for two buckets naming one group).
+__global__ void __launch_bounds__(256)
+decl_check_kernel(const uint32_t *__restrict__ ids, const uint32_t *__restrict__ len, uint32_t n,
+                  const uint32_t *__restrict__ decl, uint32_t capacity, Claim cl, uint32_t *__restrict__ err)
+{
+    __shared__ uint32_t bad;
+    const uint32_t b = blockIdx.x, e = b * kGroup + threadIdx.x;
+    if (threadIdx.x == 0) bad = 0u;
+    __syncthreads();
+    const uint32_t id = e < n ? ids[e] : ZRC4_INVALID;
+    const bool busy = id < capacity && len[e] != 0u;
+    if (busy && (id >> 8) != decl[b]) bad = 1u;
+    __syncthreads();
+    if (!bad) return;
+    if (threadIdx.x == 0) latch_fault(err, kErrGroup);
+    if (busy) {
+        unsigned long long *w = cl.word + (size_t)(id >> 8) * kClaimParts;
+        for (uint32_t p = 0; p < kClaimParts; ++p) w[p] = ((unsigned long long)cl.epoch << 32) | 0xFFFFFFFFull;
+    }
+}
 
 // One group's 64 KiB S-box image, 16 x 16 B per lane into v160..v223, issued
 // from asm and NOT waited for (the caller waits with a counted vmcnt).

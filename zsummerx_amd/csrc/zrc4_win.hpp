@@ -200,6 +200,15 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
           "s42", "s43", "s44", "s45", "s46", "s47");
 }
 
+// Declared bucket groups of a grouped window launch (zrc4_crypt_grouped_declared):
+// bucket b's group, or ZRC4_INVALID for a bucket with no busy entry.  Passed
+// by value, so it sits in the kernel-argument segment and is read with the
+// launch's other arguments: no dependent memory round trip before the image.
+constexpr uint32_t kWinMaxBuckets = 32;      // == ZRC4_WIN_MAX_GROUPS
+struct WinGroups {
+    uint32_t g[kWinMaxBuckets];
+};
+
 // Chain-bound launches with few groups: grid = 64 x groups (range batches
 // with first_slot % 256 == 0) or 64 x buckets (grouped batches) workgroups of
 // one wave.
@@ -210,17 +219,21 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
 //             builds slot -> entry, length, offset tables in LDS (in the ring,
 //             before the ring is used); the image load is issued from the
 //             first busy id's group ahead of the table build.
+//   DECL:     (kGrouped) the bucket's group comes from the caller (WinGroups):
+//             the image, x/y and claim are issued at entry, beside the
+//             bucket's entries, and a busy entry outside the declared group
+//             refuses the bucket (kErrGroup) exactly as a mixed bucket is.
 //   FRAME:    onRecv's framing walk (frame_walk, §8f row 4) of every entry in
 //             the same launch: a stream's entry by its lane 0 once the
 //             stream's bytes are decrypted; grouped entries that decrypt
 //             nothing (idle ids, length 0, idle buckets) by lane q of the
 //             bucket's workgroup q (entries q + 64r), on the raw bytes.
-template <int MODE, bool FRAME>
+template <int MODE, bool FRAME, bool DECL = false>
 __global__ void __launch_bounds__(64)
 crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const uint32_t *__restrict__ ids,
                  uint32_t first_slot, uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
                  const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity, uint32_t *__restrict__ err,
-                 uint8_t *__restrict__ sink, FrameArgs fr, Claim cl)
+                 uint8_t *__restrict__ sink, FrameArgs fr, Claim cl, WinGroups dg = WinGroups{})
 {
     Stamps ts;                                   // ZRC4_TIMING builds only (zrc4_kernels.hpp)
     stamp(ts, 0);
@@ -267,27 +280,47 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
         uint32_t idq[4], lq[4];
         uint64_t oq[4];
         bool bq[4];
+        uint32_t gw = ZRC4_INVALID;
+        if constexpr (DECL) {
+            // the declared group: image, x/y and claim leave before the
+            // bucket's entries are even read
+            gw = dg.g[wg];
+            if (gw != ZRC4_INVALID) {
+                const uint8_t *img = arena + (size_t)gw * kGroupBytes + 4u * q;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
+                sxy_g = xy[gw * 256u + kb];
+                if (lane == 0) cold = claim_part(cl, gw, q, wg);
+            }
+        }
+        // all twelve entry loads first, the checks after: a check inside the
+        // load loop would wait (vmcnt) for the declared image issued above
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t e = wg * kGroup + lane + 64u * r;
             const bool v = e < n;
-            uint32_t id = v ? ids[e] : ZRC4_INVALID;
+            idq[r] = v ? ids[e] : ZRC4_INVALID;
             lq[r] = v ? len[e] : 0u;
             oq[r] = v ? off[e] : 0u;
-            if (v && id >= capacity && id != ZRC4_INVALID) {                 // ZRC4_IDLE_SLOT pads buckets
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) te[lane + 64u * r] = ZRC4_INVALID;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (idq[r] >= capacity && idq[r] != ZRC4_INVALID) {             // ZRC4_IDLE_SLOT pads buckets
                 latch_fault(err, kErrSlotRange);
-                id = ZRC4_INVALID;
+                idq[r] = ZRC4_INVALID;
             }
-            idq[r] = id;
-            bq[r] = id != ZRC4_INVALID && lq[r] != 0u;
-            te[lane + 64u * r] = ZRC4_INVALID;
+            bq[r] = idq[r] != ZRC4_INVALID && lq[r] != 0u;
         }
         if (lane < 9) fl[lane] = 0u;
-        uint32_t gw = ZRC4_INVALID;
+        if constexpr (!DECL) {
 #pragma unroll
-        for (int r = 3; r >= 0; --r) {
-            const uint64_t bm = __builtin_amdgcn_ballot_w64(bq[r]);
-            if (bm) gw = __builtin_amdgcn_readlane(idq[r], (int)__builtin_ctzll(bm)) >> 8;
+            for (int r = 3; r >= 0; --r) {
+                const uint64_t bm = __builtin_amdgcn_ballot_w64(bq[r]);
+                if (bm) gw = __builtin_amdgcn_readlane(idq[r], (int)__builtin_ctzll(bm)) >> 8;
+            }
         }
         if constexpr (FRAME) {                        // entries that decrypt nothing: raw framing
 #pragma unroll
@@ -298,15 +331,23 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
                                fr.pkt_len);
             }
         }
-        if (gw == ZRC4_INVALID) return;                                       // idle bucket
-        gw = __builtin_amdgcn_readfirstlane(gw);
-        const uint8_t *img = arena + (size_t)gw * kGroupBytes + 4u * q;      // speculative: the first busy id's group
+        if (gw == ZRC4_INVALID) {                                             // idle bucket
+            if constexpr (DECL) {                                             // declared idle, yet a busy entry: refused
+                const bool busy = __builtin_amdgcn_ballot_w64(bq[0] | bq[1] | bq[2] | bq[3]) != 0ull;
+                if (busy && q == 0u && lane == 0) latch_fault(err, kErrGroup);
+            }
+            return;
+        }
+        if constexpr (!DECL) {
+            gw = __builtin_amdgcn_readfirstlane(gw);
+            const uint8_t *img = arena + (size_t)gw * kGroupBytes + 4u * q;  // speculative: the first busy id's group
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-            rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
-        // x/y of the stream on the same guess (no round trip after the table build)
-        sxy_g = xy[gw * 256u + kb];
-        if (lane == 0) cold = claim_part(cl, gw, q, wg);
+            for (int r = 0; r < 4; ++r)
+                rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
+            // x/y of the stream on the same guess (no round trip after the table build)
+            sxy_g = xy[gw * 256u + kb];
+            if (lane == 0) cold = claim_part(cl, gw, q, wg);
+        }
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

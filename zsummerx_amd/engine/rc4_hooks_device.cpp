@@ -9,7 +9,8 @@
 // first pinned allocation and an entry's offset is its address minus the base
 // in two's complement, so slabs anywhere in the address space share one launch.
 //
-// Every launch is a zrc4_crypt_grouped batch: entries sorted by slot, one
+// Every launch is a zrc4_crypt_grouped_declared batch (the groups built here
+// are declared with it): entries sorted by slot, one
 // 256-entry bucket per 256-slot group touched, so each bucket moves its
 // group's S-boxes as one coalesced 64 KiB image whatever subset of the group
 // the iteration touches (the kIds gather path is never used here).
@@ -110,8 +111,13 @@ struct PinnedArray {
 struct Table {
     PinnedArray<uint32_t> ids, len;
     PinnedArray<uint64_t> off;
+    std::vector<uint32_t> groups;   // each bucket's group, declared to zrc4_crypt_grouped_declared
     uint32_t n = 0;
-    void clear() { n = 0; }
+    void clear()
+    {
+        n = 0;
+        groups.clear();
+    }
     void push(uint32_t id, uint64_t o, uint32_t l)
     {
         if (n == ids.cap || n == off.cap || n == len.cap) {
@@ -174,6 +180,7 @@ void buildGrouped(Table &t, std::vector<Entry> &es, FrameTable *ft = nullptr)
         if (g != cur) {
             while (t.n % ZRC4_GROUP_SLOTS) push(ZRC4_IDLE_SLOT, 0, 0, nullptr);
             cur = g;
+            t.groups.push_back(g);
         }
         push(e.slot, e.off, e.len, &e);
     }
@@ -410,7 +417,8 @@ public:
         buildGrouped(tt_, es_, &ft_);
         zrc4_frame_args fa{ft_.off.p, ft_.len.p, bound, Rc4Frame::kMaxPackets, ft_.npk.p, ft_.used.p,
                            ft_.status.p, ft_.pkt.p};
-        rc = zrc4_crypt_grouped_frame(ctx_, tt_.ids.p, base_, tt_.off.p, tt_.len.p, tt_.n, &fa, sA_);
+        rc = zrc4_crypt_grouped_declared(ctx_, tt_.ids.p, tt_.groups.data(), base_, tt_.off.p, tt_.len.p, tt_.n,
+                                         &fa, sA_);
         if (rc != ZRC4_OK) return rc;
         ++tailLaunches_;
         if ((rc = zrc4_sync(ctx_, sA_)) != ZRC4_OK) return rc;
@@ -468,7 +476,8 @@ private:
     {
         if (es.empty()) return ZRC4_OK;
         buildGrouped(tt_, es);
-        int rc = zrc4_crypt_grouped(ctx_, tt_.ids.p, base_, tt_.off.p, tt_.len.p, tt_.n, sA_);
+        int rc = zrc4_crypt_grouped_declared(ctx_, tt_.ids.p, tt_.groups.data(), base_, tt_.off.p, tt_.len.p, tt_.n,
+                                             nullptr, sA_);
         if (rc != ZRC4_OK) return rc;
         ++tailLaunches_;
         return zrc4_sync(ctx_, sA_);
@@ -607,7 +616,8 @@ private:
         hungry_.swap(keep);
         if (rs_.empty()) return ZRC4_OK;
         buildGrouped(R.t, rs_);
-        int rc = zrc4_crypt_grouped(ctx_, R.t.ids.p, base_, R.t.off.p, R.t.len.p, R.t.n, sB_);
+        int rc = zrc4_crypt_grouped_declared(ctx_, R.t.ids.p, R.t.groups.data(), base_, R.t.off.p, R.t.len.p,
+                                             R.t.n, nullptr, sB_);
         if (rc != ZRC4_OK) {
             // nothing queued: the levels go back (pend > gen with no refill in
             // flight would make cryptReservoir wait for bytes that never come)
