@@ -323,7 +323,7 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
     B = algorithmic_bytes(S, L)
     achieved = B / (kern_avg_ms * 1e-3) / 1e9
     ids = getattr(args, "ids", "range")
-    traffic = load_traffic(args.workload if ids == "range" else f"{args.workload}-{ids}")
+    traffic, traffic_src = load_traffic(args.workload if ids == "range" else f"{args.workload}-{ids}")
     return {
         "metric": METRIC,
         "value": round(value, 3),
@@ -353,6 +353,7 @@ def build_result(args, ws, S, L, R, tmax, kern_avg_ms, kern_ms, total_payload):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": kernel_name(S, getattr(args, "ids", "range")),
                      "algorithmic_bytes_per_launch": B,
                      "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
@@ -404,15 +405,20 @@ def kernel_name(S: int, ids: str = "range") -> str:
 
 
 def load_traffic(workload: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any:
+    (bytes, where they come from).  The PMC passes run in their own rocprofv3
+    processes (scripts/pmc_traffic.sh), never inside this bench run."""
     p = ROOT / "profiles" / f"pmc_{workload}.json"
     if not p.exists():
-        return None
+        return None, None
     try:
         d = json.loads(p.read_text())
-        return d.get("hbm_bytes_per_launch")
+        src = (f"profiles/pmc_{workload}.json (round {d.get('round', '?')}, builder's rocprofv3 FETCH_SIZE + "
+               f"WRITE_SIZE passes over bench.py --workload {d.get('workload', workload)}; kernel "
+               f"{d.get('kernel', '?')}; not measured in this run)")
+        return d.get("hbm_bytes_per_launch"), src
     except Exception:
-        return None
+        return None, None
 
 
 # ------------------------------------------------------------- CPU baseline

@@ -608,7 +608,7 @@ def test_grouped_ids_mixed_bucket_is_refused(built, torch_cuda):
 
 
 @pytest.mark.parametrize("nb,variant", [(20, None), (100, None), (200, None), (700, None), (1600, None),
-                                        (1600, "preclaim1")])
+                                        (1600, "preclaim1"), (5000, None)])
 def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb, variant):
     """The cross-bucket half of the zrc4_crypt_grouped contract: two buckets
     of one call name the same group (disjoint slots of it).  The call reports
@@ -621,7 +621,11 @@ def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb, variant
     bucket's group a group ahead; from 3 buckets per workgroup (1600) the
     first 64 of a workgroup in its prologue instead -- the preclaim1 test
     build pre-claims only the first, so the contested buckets meet across
-    both paths).  Every entry is checked (states read back in one copy)."""
+    both paths).  5000 short buckets (1-6 entries): about 10 buckets per
+    workgroup, so the prologue pre-claims in two rounds of 8 and the second
+    contested bucket (4998, the 10th of its workgroup) is claimed in the
+    second round.  Every entry is checked (states read back in
+    one copy)."""
     torch = torch_cuda
     from zsummerx_amd._capi import IDLE_SLOT
     rng = np.random.default_rng(500 + nb)
@@ -646,12 +650,13 @@ def test_grouped_cross_bucket_conflict_is_refused(built, torch_cuda, nb, variant
             ids[256 * b: 256 * b + 128] = contested * 256 + half[:128]
         else:
             g = int(groups[b if b < dup_b else b - 1])
-            k = int(rng.integers(1, 257))
+            k = int(rng.integers(1, 257 if nb <= 2000 else 7))
             ids[256 * b + rng.permutation(256)[:k]] = g * 256 + rng.permutation(256)[:k]
     busy = ids != IDLE_SLOT
-    L = np.where(busy, rng.integers(1, 500, ids.size), 0).astype(np.uint32)
-    off = np.arange(ids.size, dtype=np.uint64) * 512
-    data = rng.integers(0, 256, ids.size * 512, dtype=np.uint8)
+    span = 512 if nb <= 2000 else 64
+    L = np.where(busy, rng.integers(1, span - 12, ids.size), 0).astype(np.uint32)
+    off = np.arange(ids.size, dtype=np.uint64) * span
+    data = rng.integers(0, 256, ids.size * span, dtype=np.uint8)
     from zsummerx_amd import build
     with Context(0, cap, lib=None if variant is None else build.PKG / f"libzrc4_{variant}.so") as c:
         c.ksa_range(0, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
@@ -1005,6 +1010,57 @@ def test_reservoir_failed_tail_loses_position_until_reseeded(built, monkeypatch)
         assert rc == 0 and out == pyoracle.Rc4(b"lost-slot").encryption(bytes(100))
         rc, out = call(1, 50)
         assert rc == 0 and out == ref1.encryption(bytes(50))
+    finally:
+        if ks:
+            lib.zrc4_ks_destroy(ks)
+        lib.zrc4_destroy(ctx)
+
+
+def test_reservoir_failed_tail_loses_every_slot_of_the_call(built, monkeypatch):
+    """a failed tail marks EVERY slot with len > 0 of the call
+    lost, including one served entirely from its ring (its span was already
+    crypted on the host when the tail failed).  Slot A's first call is a tail
+    (tail 1) and queues its refill; the two-slot call [A: 16 bytes, B: 64]
+    serves A from its ring and needs a tail for B (tail 2, injected failure).
+    Afterwards both A and B return ZRC4_ERR_STATE until reseeded; reseeded,
+    both give the reference bytes again."""
+    import ctypes as C
+    from zsummerx_amd import _capi, build
+    lib = _capi.load(build.PKG / "libzrc4_testhooks.so")
+    monkeypatch.setenv("ZRC4_KS_FAIL_TAIL_AFTER", "2")
+    ctx, ks = C.c_void_p(), C.c_void_p()
+    assert lib.zrc4_create(C.byref(ctx), 0, 256) == 0
+    try:
+        assert lib.zrc4_ks_create(ctx, 4096, C.byref(ks)) == 0
+        for slot, key in ((0, b"slot-a"), (1, b"slot-b")):
+            assert lib.zrc4_ks_make_sbox(ks, slot, key, len(key)) == 0
+
+        def call(slots, lens):
+            bufs = [(C.c_uint8 * n)() for n in lens]
+            ids = (C.c_uint32 * len(slots))(*slots)
+            ptrs = (C.c_void_p * len(slots))(*[C.cast(b, C.c_void_p) for b in bufs])
+            ln = (C.c_uint32 * len(slots))(*lens)
+            return lib.zrc4_ks_crypt(ks, ids, ptrs, ln, len(slots)), [bytes(b) for b in bufs]
+
+        def ring_bytes():
+            st = (C.c_uint64 * 6)()
+            assert lib.zrc4_ks_stats(ks, st) == 0
+            return st[0]
+
+        refa = pyoracle.Rc4(b"slot-a")
+        rc, (out,) = call([0], [64])                   # tail 1; A's refill is queued
+        assert rc == 0 and out == refa.encryption(bytes(64))
+        r0 = ring_bytes()
+        rc, _ = call([0, 1], [16, 64])                 # A from its ring, B's tail fails (tail 2)
+        assert rc != 0
+        assert ring_bytes() - r0 == 16                 # A was served from its ring
+        for slot in (0, 1):
+            rc, (out,) = call([slot], [32])
+            assert rc == -9 and out == bytes(32), slot  # ZRC4_ERR_STATE, nothing crypted
+        for slot, key in ((0, b"slot-a"), (1, b"slot-b")):
+            assert lib.zrc4_ks_make_sbox(ks, slot, key, len(key)) == 0
+            rc, (out,) = call([slot], [100])
+            assert rc == 0 and out == pyoracle.Rc4(key).encryption(bytes(100)), slot
     finally:
         if ks:
             lib.zrc4_ks_destroy(ks)

@@ -16,6 +16,7 @@
 #include "win64_loop.hpp"
 #include "win12_loop.hpp"
 #include "win_var.hpp"
+#include "win_repair.hpp"
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 constexpr int MAXN = (int)zrc4::kWinRing;   // keystream ring per stream (bytes)
@@ -648,7 +649,46 @@ win12_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uin
     }
 }
 
-
+// v13: repaired windows (tools/ubench/win_repair.hpp, compiled HIP), W = 16,
+// 4 streams per wave; compare with mode 1 (the product rules in compiled HIP)
+// and mode 6 (the product asm loop).
+__global__ void __launch_bounds__(64)
+win13_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+             uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int W = 16, SPW = 4;
+    __shared__ __attribute__((aligned(1024))) uint32_t Mlo[SPW * 256];
+    __shared__ __attribute__((aligned(1024))) uint32_t Mhi[SPW * 256];
+    __shared__ __attribute__((aligned(MAXN))) uint8_t Ring[SPW * MAXN];
+    __shared__ __attribute__((aligned(256))) uint8_t Sb[SPW * 256];
+    const uint32_t lane = threadIdx.x, l = lane % W, g = lane / W;
+    const int s = blockIdx.x * SPW + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        S[l * (256 / W) + k] = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        Mlo[g * 256 + l * (256 / W) + k] = 0;
+        Mhi[g * 256 + l * (256 / W) + k] = 0;
+    }
+    const uint32_t sxy = live ? xy_in[s] : 0;
+    __syncthreads();
+    uint32_t xa = ((sxy & 0xFFu) + 1u) & 0xFFu, y = sxy >> 8, tag = 1, rp = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint32_t nw = zrc4::win_repair_windows(xa, y, tag, live ? (uint32_t)N : 0u, rp, l, S, Mlo + g * 256,
+                                                 Mhi + g * 256, R, MAXN);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((xa - 1) & 255) | ((y & 255) << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = nw;
+        }
+    }
+}
 
 
 // v7: one stream per wave, W = 64 (zrc4::win64_windows).
@@ -756,7 +796,8 @@ static void run(int ns, int N, int reps)
     std::vector<float> ms;
     for (int r = 0; r < reps; ++r) {
         CHECK(hipEventRecord(e0));
-        if constexpr (V3 == 12) win12_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        if constexpr (V3 == 13) win13_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if constexpr (V3 == 12) win12_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if constexpr (V3 == 11) win11_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if constexpr (V3 == 10) win10_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if constexpr (V3 == 9) win9_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
@@ -806,7 +847,8 @@ int main(int argc, char **argv)
     const int wpb = argc > 4 ? atoi(argv[4]) : 1;
     if (N > MAXN || N % 16) { printf("bytes must be a multiple of 16 and <= %d\n", MAXN); return 1; }
     const int v3 = argc > 5 ? atoi(argv[5]) : 1;
-    if (v3 == 12) run<16, 1, 12>(ns, N, 20);
+    if (v3 == 13) run<16, 1, 13>(ns, N, 20);
+    else if (v3 == 12) run<16, 1, 12>(ns, N, 20);
     else if (v3 == 11) run<16, 1, 11>(ns, N, 20);
     else if (v3 == 10) run<16, 1, 10>(ns, N, 20);
     else if (v3 == 9) run<16, 1, 9>(ns, N, 20);
