@@ -2,8 +2,9 @@
 
 1. The asm-issued-load discipline: no instruction may read
    or write a VGPR while a full-EXEC VMEM load into it can still be in
-   flight (on the prefetching persistent kernels: any VMEM load, whatever
-   the EXEC mask -- the grouped claim is issued by lane 0 alone).  tools/vmem_hazard_check.py proves it on the product library's
+   flight (on the prefetching persistent kernels and the grouped window
+   kernels: any VMEM load, whatever the EXEC mask -- the grouped claim is
+   issued by lane 0 alone).  tools/vmem_hazard_check.py proves it on the product library's
    code object, and must flag the removed round-2 "sink load in place of each
    store" line loop (the variant that faulted the GPU in round 3), which
    tools/gen_line_loop.py --hazard-demo regenerates into a scratch directory.
@@ -35,6 +36,7 @@ pytestmark = pytest.mark.skipif(not LLVM_OK, reason="ROCm LLVM tools not found")
 PINNED = set(range(40, 104)) | set(range(148, 152)) | set(range(160, 224))
 PREFETCHING = ("crypt_stream_kernelILb1ELb0ELb0E", "crypt_stream_kernelILb1ELb1ELb0E",   # range / grouped
                "crypt_stream_kernelILb1ELb0ELb1E", "crypt_stream_kernelILb1ELb1ELb1E")   # framed
+WIN_GROUPED = ("crypt_win_kernelILi2E",)      # the window kernel's claim, issued from asm by lane 0 (r05)
 
 
 def _check_one(item):
@@ -44,7 +46,7 @@ def _check_one(item):
     # with lane 0 alone: there every load is tracked, whatever the EXEC mask
     # (ADVICE r04), so a compiler copy of the claim's register before its
     # wait would be flagged too
-    partial = any(k in name for k in PREFETCHING)
+    partial = any(k in name for k in PREFETCHING + WIN_GROUPED)
     hz, _ = vh.check_function(name, insns, debug=dbg, track_partial=partial, max_states=1500000)
     idx = {i.addr: i for i in insns}
     pinned = [a for a in dbg.get("loads", {}) if vh.vmem_dest(idx[a]) & PINNED]

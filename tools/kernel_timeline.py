@@ -89,9 +89,9 @@ def main():
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--placement", action="store_true",
                     help="per-wave chain cycles/byte against where the wave ran (XCC, SE, SH, CU, SIMD)")
-    ap.add_argument("--ids", choices=("range", "grouped"), default="range",
+    ap.add_argument("--ids", choices=("range", "grouped", "declared"), default="range",
                     help="grouped: slots permuted inside each group, groups in random order (bench.py --ids grouped) "
-                         "through zrc4_crypt_grouped")
+                         "through zrc4_crypt_grouped; declared: the same through zrc4_crypt_grouped_declared")
     ap.add_argument("--active-waves", type=int, default=4,
                     help="only the first k waves of every 256-session group get payload (len 0 for the rest): "
                          "the chain rate at k waves per CU")
@@ -122,15 +122,16 @@ def main():
         koff = torch.arange(n, dtype=torch.int64, device=dev) * 16
         pay = torch.from_numpy(synth.payload(0, n * L, threads=8)).to(dev)
         perm = np.arange(n, dtype=np.int64)
-        if args.ids == "grouped":
+        bgroups = []
+        if args.ids != "range":
+            if S % 256:
+                raise SystemExit("grouped modes need whole groups")
             rng = np.random.default_rng(77)
             for b in range(R):
-                G = -(-S // 256)
-                pos = 0
-                for g in rng.permutation(G):
-                    lo, hi = b * S + g * 256, min(b * S + (g + 1) * 256, (b + 1) * S)
-                    perm[b * S + pos: b * S + pos + (hi - lo)] = lo + rng.permutation(hi - lo)
-                    pos += hi - lo
+                order = rng.permutation(S // 256)
+                bgroups.append(np.ascontiguousarray((b * S // 256 + order).astype(np.uint32)))
+                for k, g in enumerate(order):
+                    perm[b * S + 256 * k: b * S + 256 * (k + 1)] = b * S + g * 256 + rng.permutation(256)
         ids = torch.from_numpy(perm.astype(np.int32)).to(dev)
         off = torch.from_numpy(perm * L).to(dev)
         lnh = np.full(n, L, dtype=np.int32)
@@ -147,7 +148,13 @@ def main():
         torch.cuda.synchronize()
         for i in range(args.launches):
             b = i % R
-            if args.ids == "grouped":
+            if args.ids == "declared":
+                _capi.check(lib.zrc4_crypt_grouped_declared(h, C.c_void_p(ids.data_ptr() + 4 * b * S),
+                                                            C.c_void_p(bgroups[b].ctypes.data),
+                                                            C.c_void_p(pay.data_ptr()),
+                                                            C.c_void_p(off.data_ptr() + 8 * b * S),
+                                                            C.c_void_p(ln.data_ptr() + 4 * b * S), S, None, st))
+            elif args.ids == "grouped":
                 _capi.check(lib.zrc4_crypt_grouped(h, C.c_void_p(ids.data_ptr() + 4 * b * S),
                                                    C.c_void_p(pay.data_ptr()), C.c_void_p(off.data_ptr() + 8 * b * S),
                                                    C.c_void_p(ln.data_ptr() + 4 * b * S), S, st))

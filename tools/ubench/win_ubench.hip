@@ -691,6 +691,48 @@ win13_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uin
 }
 
 
+// v15: the product loop (zrc4::win_windows) with 2 streams per wave (lanes
+// 32-63 idle), so 4 096 streams take 2 048 waves: 2 per SIMD instead of 1.
+// Does a second wave on each SIMD hide the loop's LDS round trips?
+__global__ void __launch_bounds__(64)
+win15_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+             uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int W = 16, SPW = 4, LIVE = 2;
+    __shared__ __attribute__((aligned(1024))) uint32_t Mk[SPW * 256];
+    __shared__ __attribute__((aligned(MAXN))) uint8_t Ring[SPW * MAXN];
+    __shared__ __attribute__((aligned(512))) uint8_t Sb[SPW * 512];
+    const uint32_t lane = threadIdx.x, l = lane % W, g = lane / W;
+    const int s = blockIdx.x * LIVE + (int)g;
+    const bool live = g < (uint32_t)LIVE && s < nstreams;
+    uint8_t *S = Sb + g * 512;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        const uint8_t v = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        S[l * (256 / W) + k] = v;
+        S[256 + l * (256 / W) + k] = v;
+        M[l * (256 / W) + k] = 0;
+    }
+    const uint32_t sxy = live ? xy_in[s] : 0;
+    __syncthreads();
+    zrc4::WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    zrc4::win_windows(w, live ? (uint32_t)N : 0u, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
+                      (uint32_t)(uintptr_t)R);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((w.xa - 1) & 255) | ((w.y & 255) << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = (w.v >> 8) - 1;
+        }
+    }
+}
+
 // v7: one stream per wave, W = 64 (zrc4::win64_windows).
 __global__ void __launch_bounds__(64)
 win7_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
@@ -796,7 +838,8 @@ static void run(int ns, int N, int reps)
     std::vector<float> ms;
     for (int r = 0; r < reps; ++r) {
         CHECK(hipEventRecord(e0));
-        if constexpr (V3 == 13) win13_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        if constexpr (V3 == 15) win15_kernel<<<(ns + 1) / 2, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if constexpr (V3 == 13) win13_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if constexpr (V3 == 12) win12_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if constexpr (V3 == 11) win11_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if constexpr (V3 == 10) win10_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
@@ -847,7 +890,8 @@ int main(int argc, char **argv)
     const int wpb = argc > 4 ? atoi(argv[4]) : 1;
     if (N > MAXN || N % 16) { printf("bytes must be a multiple of 16 and <= %d\n", MAXN); return 1; }
     const int v3 = argc > 5 ? atoi(argv[5]) : 1;
-    if (v3 == 13) run<16, 1, 13>(ns, N, 20);
+    if (v3 == 15) run<16, 1, 15>(ns, N, 20);
+    else if (v3 == 13) run<16, 1, 13>(ns, N, 20);
     else if (v3 == 12) run<16, 1, 12>(ns, N, 20);
     else if (v3 == 11) run<16, 1, 11>(ns, N, 20);
     else if (v3 == 10) run<16, 1, 10>(ns, N, 20);

@@ -44,8 +44,17 @@ struct zrc4_ctx {
     hipStream_t stream;     // private stream for the host entry points
     unsigned long long *claim;   // grouped launches' (group, part) claim words (zrc4::Claim), zeroed
     uint32_t epoch;              // the last grouped launch's claim tag
-    uint32_t *d_decl;            // declared bucket groups of a large declared launch (decl_check_kernel)
-    uint32_t d_decl_cap;         // ... its capacity in buckets
+    // Declared bucket groups of large declared launches (decl_check_kernel
+    // reads them zero-copy): a ring of coherent pinned buffers, each reused
+    // once the check kernel that read it has run (its event).  A pageable
+    // hipMemcpyAsync here blocked the host until the stream drained: +4.7 us
+    // per cfg3 call back to back (profiles/r05/ab_ids_modes.log).
+    static constexpr int kDeclRing = 4;
+    uint32_t *h_decl[kDeclRing];
+    uint32_t h_decl_cap[kDeclRing];
+    hipEvent_t decl_ev[kDeclRing];
+    bool decl_ev_live[kDeclRing];
+    uint32_t decl_next;
 };
 
 namespace {
@@ -153,17 +162,27 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
     if (decl && mode == zrc4::kGrouped && !decl_trusted) {
         // check the declared groups before the crypt launch (stream-ordered):
         // a disagreeing bucket's groups are claimed under this launch's epoch
-        if (grid > c->d_decl_cap) {
-            if (c->d_decl) (void)hipFree(c->d_decl);
-            c->d_decl = nullptr;
-            c->d_decl_cap = 0;
-            if (hipMalloc(&c->d_decl, (size_t)grid * 4u) != hipSuccess) return ZRC4_ERR_OUT_OF_MEMORY;
-            c->d_decl_cap = grid;
+        const int k = (int)(c->decl_next++ % (uint32_t)zrc4_ctx::kDeclRing);
+        if (c->decl_ev_live[k]) ZRC4_TRY(hipEventSynchronize(c->decl_ev[k]));    // its last reader has run
+        if (!c->decl_ev[k] && hipEventCreateWithFlags(&c->decl_ev[k], hipEventDisableTiming) != hipSuccess)
+            return ZRC4_ERR_HIP;
+        if (grid > c->h_decl_cap[k]) {
+            if (c->h_decl[k]) (void)hipHostFree(c->h_decl[k]);
+            c->h_decl[k] = nullptr;
+            c->h_decl_cap[k] = 0;
+            uint32_t want = 1024u;
+            while (want < grid) want <<= 1;
+            void *p = nullptr;
+            if (hipHostMalloc(&p, (size_t)want * 4u, hipHostMallocCoherent) != hipSuccess) return ZRC4_ERR_OUT_OF_MEMORY;
+            c->h_decl[k] = static_cast<uint32_t *>(p);
+            c->h_decl_cap[k] = want;
         }
-        ZRC4_TRY(hipMemcpyAsync(c->d_decl, decl, (size_t)grid * 4u, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(zrc4::decl_check_kernel, dim3(grid), blk, 0, s, ids, len, n, c->d_decl, c->capacity,
+        memcpy(c->h_decl[k], decl, (size_t)grid * 4u);
+        hipLaunchKernelGGL(zrc4::decl_check_kernel, dim3(grid), blk, 0, s, ids, len, n, c->h_decl[k], c->capacity,
                            cl, c->err);
         if (hipGetLastError() != hipSuccess) return ZRC4_ERR_LAUNCH;
+        ZRC4_TRY(hipEventRecord(c->decl_ev[k], s));
+        c->decl_ev_live[k] = true;
     }
     // Few whole groups: half-group workgroups, one per CU (2 waves per CU).
     // A grouped bucket's slots may sit in either half whatever its entry
@@ -326,7 +345,11 @@ int zrc4_destroy(zrc4_ctx *c)
     if (c->xy) (void)hipFree(c->xy);
     if (c->sink) (void)hipFree(c->sink);
     if (c->claim) (void)hipFree(c->claim);
-    if (c->d_decl) (void)hipFree(c->d_decl);
+    for (int k = 0; k < zrc4_ctx::kDeclRing; ++k) {
+        if (c->decl_ev_live[k]) (void)hipEventSynchronize(c->decl_ev[k]);   // a check kernel may still read h_decl
+        if (c->decl_ev[k]) (void)hipEventDestroy(c->decl_ev[k]);
+        if (c->h_decl[k]) (void)hipHostFree(c->h_decl[k]);
+    }
     if (c->err) (void)hipHostFree(c->err);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);

@@ -79,6 +79,35 @@ __device__ __forceinline__ unsigned long long claim_part(const Claim &cl, uint32
                                  __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The same exchange issued from asm by lane 0 with the rest of the wave
+// masked off: the compiler neither sees nor counts it, so its waits for older
+// loads do not also wait for the atomic's round trip (a lane-0-only atomic in
+// compiler code sits on a divergent path, and the waitcnt pass then drains
+// with vmcnt(0) at the next wait).  The caller retires it explicitly
+// (claim_wait) before reading the answer; lane 0 must be active here.
+__device__ __forceinline__ unsigned long long claim_part_async(const Claim &cl, uint32_t g, uint32_t part,
+                                                               uint32_t bucket)
+{
+    unsigned long long old;
+    uint64_t sv;
+    const unsigned long long v = ((unsigned long long)cl.epoch << 32) | bucket;
+    unsigned long long *addr = cl.word + (size_t)g * kClaimParts + part;
+    asm volatile("s_mov_b64 %[sv], exec\n\t"
+                 "s_mov_b64 exec, 1\n\t"
+                 "global_atomic_swap_x2 %[old], %[a], %[v], off sc0\n\t"
+                 "s_mov_b64 exec, %[sv]"
+                 : [old] "=&v"(old), [sv] "=&s"(sv)
+                 : [a] "v"(addr), [v] "v"(v)
+                 : "memory");
+    return old;
+}
+
+// Retire every VMEM op in flight, claim_part_async's answer included.
+__device__ __forceinline__ void claim_wait(unsigned long long &old)
+{
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(old) :: "memory");
+}
+
 __device__ __forceinline__ bool claim_lost(const Claim &cl, unsigned long long old)
 {
     return (uint32_t)(old >> 32) == cl.epoch;

@@ -256,6 +256,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
     uint32_t rows[4];
     uint32_t sxy, sxy_g;                                                   // sxy_g: kGrouped's x/y on the guess
     unsigned long long cold = 0;                                           // kGrouped: the claim of column q (Claim)
+    uint32_t gclaim = 0;                                                   // kGrouped: the group claimed
     bool bad = false;                                                      // kGrouped: the bucket breaks the contract
     if constexpr (MODE == kRange) {
         const uint32_t e = wg * kGroup + kb;
@@ -281,21 +282,8 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
         uint64_t oq[4];
         bool bq[4];
         uint32_t gw = ZRC4_INVALID;
-        if constexpr (DECL) {
-            // the declared group: image, x/y and claim leave before the
-            // bucket's entries are even read
-            gw = dg.g[wg];
-            if (gw != ZRC4_INVALID) {
-                const uint8_t *img = arena + (size_t)gw * kGroupBytes + 4u * q;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
-                sxy_g = xy[gw * 256u + kb];
-                if (lane == 0) cold = claim_part(cl, gw, q, wg);
-            }
-        }
-        // all twelve entry loads first, the checks after: a check inside the
-        // load loop would wait (vmcnt) for the declared image issued above
+        // all twelve entry loads first, the checks after (a check inside the
+        // load loop would wait for every load issued before it)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t e = wg * kGroup + lane + 64u * r;
@@ -303,6 +291,22 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             idq[r] = v ? ids[e] : ZRC4_INVALID;
             lq[r] = v ? len[e] : 0u;
             oq[r] = v ? off[e] : 0u;
+        }
+        if constexpr (DECL) {
+            // the declared group: image, x/y and claim leave right behind the
+            // entries, in the same round trip (without it they wait for the
+            // entries' ids); the entry checks wait for the entries only, and
+            // the claim (asm, uncounted by the compiler) for nothing before
+            // the first XOR pass
+            // (an idle bucket reads group 0's image and drops it: loads on
+            // every path keep the compiler's counted waits exact)
+            gw = dg.g[wg];
+            const uint32_t gl = gw != ZRC4_INVALID ? gw : 0u;
+            const uint8_t *img = arena + (size_t)gl * kGroupBytes + 4u * q;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
+            sxy_g = xy[gl * 256u + kb];
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) te[lane + 64u * r] = ZRC4_INVALID;
@@ -346,8 +350,8 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
                 rows[r] = *reinterpret_cast<const uint32_t *>(img + (size_t)(lane + 64u * r) * 256u);
             // x/y of the stream on the same guess (no round trip after the table build)
             sxy_g = xy[gw * 256u + kb];
-            if (lane == 0) cold = claim_part(cl, gw, q, wg);
         }
+        gclaim = gw;
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -373,41 +377,63 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
     uint8_t *img = arena + (size_t)(slot >> 8) * kGroupBytes + 4u * q;
     uint8_t *msg = payload + O;
     const bool aligned = ((uintptr_t)msg & 15u) == 0u;
-
-    // payload prefetch of chunk 0 (aligned messages: whole 16-byte units).
-    // kGrouped: issued before the claim's answer is waited for (reads of the
-    // caller's entries only; a refused bucket drops them).
-    uint4 pre[kWinUnits];
+    uint8_t *S = Sb + b * 256u;
+    uint32_t *M = Mk + b * 256u;
+    uint8_t *R = Ring + b * kWinRing;
+    // the S-boxes into LDS (the wave's 4 streams share every dword of the
+    // image column) and the markers cleared
+    auto fill = [&]() {
 #pragma unroll
-    for (uint32_t u = 0; u < kWinUnits; ++u) {
-        const uint32_t pos = 16u * (l + kWinLanes * u);
-        if (aligned && pos + 16u <= L) pre[u] = *reinterpret_cast<const uint4 *>(msg + pos);
-    }
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t kk = lane + 64u * r;
+#pragma unroll
+            for (uint32_t s4 = 0; s4 < 4; ++s4) {
+                const uint8_t v = (uint8_t)(rows[r] >> (8 * s4));
+                Sb[s4 * 256u + kk] = v;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) reinterpret_cast<uint4 *>(Mk)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
+    };
     if constexpr (MODE == kGrouped) {
         if (bad) {
+            claim_wait(cold);                                                 // (no load left in flight at exit)
             if (lane == 0) latch_fault(err, kErrGroup);
             return;
         }
         sxy = valid ? sxy_g : 0u;
-        if (!__builtin_amdgcn_ballot_w64(valid)) return;
-        __syncthreads();                                                      // tables read before the ring is used
+        if (!__builtin_amdgcn_ballot_w64(valid)) {
+            claim_wait(cold);
+            return;
+        }
+        // The fill goes before the payload prefetch here: its addresses come
+        // from the slot table (a second round trip), and with the prefetch
+        // issued first the compiler's wait for the image column (older, on
+        // a path the per-lane prefetch branches join) drained the prefetch
+        // too, a round trip on the way to the first window (r05 timeline:
+        // prologue 3.84 vs 2.24 us range, profiles/r05/tl1/).
+        fill();
     }
 
-    uint8_t *S = Sb + b * 256u;
-    uint32_t *M = Mk + b * 256u;
-    uint8_t *R = Ring + b * kWinRing;
+    // payload prefetch of chunk 0 (aligned messages: whole 16-byte units).
+    // kGrouped: issued before the claim's answer is waited for (reads of the
+    // caller's entries only; a refused bucket drops them), on every lane
+    // (units past the message read the lane's sink bytes) so that the
+    // compiler's wait for x/y below counts exactly and leaves the claim --
+    // issued right after, from asm -- in flight until the first XOR pass.
+    uint4 pre[kWinUnits];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint32_t kk = lane + 64u * r;
-#pragma unroll
-        for (uint32_t s4 = 0; s4 < 4; ++s4) {
-            const uint8_t v = (uint8_t)(rows[r] >> (8 * s4));
-            Sb[s4 * 256u + kk] = v;
-        }
+    for (uint32_t u = 0; u < kWinUnits; ++u) {
+        const uint32_t pos = 16u * (l + kWinLanes * u);
+        const bool use = aligned && pos + 16u <= L;
+        if constexpr (MODE == kGrouped)
+            pre[u] = *reinterpret_cast<const uint4 *>(use ? msg + pos : sink + 16u * lane);
+        else if (use)
+            pre[u] = *reinterpret_cast<const uint4 *>(msg + pos);
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) reinterpret_cast<uint4 *>(Mk)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
+    if constexpr (MODE == kGrouped) cold = claim_part_async(cl, gclaim, q, wg);
+    if constexpr (MODE != kGrouped) fill();
+    __syncthreads();                                 // (grouped: also the tables read before the ring is used)
     stamp(ts, 1);
 
     const uint32_t sb = (uint32_t)(uintptr_t)S, mb = (uint32_t)(uintptr_t)M, rb = (uint32_t)(uintptr_t)R;
@@ -429,10 +455,12 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             // written yet (the windows run in LDS), so its round trip hides
             // under the first chunk's keystream.  lost: another bucket of
             // this launch holds column q; store nothing.
-            if (c0 == 0u &&
-                claim_lost(cl, ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(cold >> 32))) << 32)) {
-                if (lane == 0) latch_fault(err, kErrGroup);
-                return;
+            if (c0 == 0u) {
+                claim_wait(cold);        // (the XOR pass below waits for the payload prefetch anyway)
+                if (claim_lost(cl, ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(cold >> 32))) << 32)) {
+                    if (lane == 0) latch_fault(err, kErrGroup);
+                    return;
+                }
             }
         }
         // XOR pass of [c0, c1): whole 16-byte units from the prefetch, bytes
