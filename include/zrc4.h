@@ -149,14 +149,17 @@ int zrc4_crypt_grouped(zrc4_ctx *ctx, const uint32_t *ids, uint8_t *payload,
  * >= capacity / 256 returns ZRC4_ERR_INVALID_ARG and launches nothing.
  * Semantics are zrc4_crypt_grouped's, plus one refusal: a bucket with a busy
  * entry outside its declared group is refused (ZRC4_ERR_GROUP, nothing of it
- * written).  Why: with at most 32 buckets (the 16-lanes-per-stream kernel,
- * where the launch is one keystream chain long) the groups travel in the
- * kernel arguments, so each bucket's state image is loaded at kernel entry
- * instead of after a dependent read of the bucket's ids.  With more buckets
- * the declared groups are checked by a short kernel on the same stream just
- * before the crypt launch; a disagreeing bucket's own ids then also block
- * the groups they name, so another bucket naming one of those groups is
- * refused too (the rule for two buckets naming one group).  frame: NULL for
+ * written).  Why: with at most 256 buckets (at most one bucket per CU, where
+ * the launch is one keystream chain long) the groups travel in the kernel
+ * arguments, so each bucket's state image is loaded with its entries instead
+ * of after a dependent read of the bucket's ids.  With more buckets the
+ * declared groups are checked by a short kernel on the same stream just
+ * before the crypt launch (it reads them from pinned memory the call fills);
+ * a disagreeing bucket's own ids then also block the groups they name, so
+ * another bucket naming one of those groups is refused too (the rule for two
+ * buckets naming one group).  Callers that build their buckets themselves
+ * gain nothing from the declaration above 256 buckets: there the persistent
+ * kernel already prefetches each bucket's ids a bucket ahead.  frame: NULL for
  * no framing, else zrc4_crypt_grouped_frame's framing (below).  Device
  * pointers apart from bucket_group; asynchronous. */
 struct zrc4_frame_args;

@@ -64,13 +64,14 @@ def _check_states(c, ob, cap):
     assert bad.size == 0, bad[:8]
 
 
-@pytest.mark.parametrize("nb,trunc,idle", [(16, 0, 0), (27, 11, 0.2), (32, 0, 0), (100, 0, 0.1), (300, 37, 0),
-                                           (700, 0, 0.05)])
+@pytest.mark.parametrize("nb,trunc,idle", [(16, 0, 0), (27, 11, 0.2), (32, 0, 0), (100, 0, 0.1), (200, 5, 0.1),
+                                           (256, 0, 0), (300, 37, 0), (700, 0, 0.05)])
 def test_declared_bit_exact(built, torch_cuda, nb, trunc, idle):
     """nb <= 32: the window kernel with the groups in its arguments (16 and 32
-    buckets: every column of a bucket on one XCD; 27: spread); 100 / 300 /
-    700: half-group, whole-group and persistent kernels behind the declared
-    check.  Idle buckets declared ZRC4_IDLE_SLOT, a truncated last bucket,
+    buckets: every column of a bucket on one XCD; 27: spread); 100: the
+    half-group kernel and 200 / 256 the whole-group kernel, the groups in
+    their arguments too (crypt_decl_kernel); 300 / 700: the persistent kernel
+    behind the declared check.  Idle buckets declared ZRC4_IDLE_SLOT, a truncated last bucket,
     two calls in a row, every state checked (slots outside the calls keep
     theirs)."""
     torch = torch_cuda
@@ -102,7 +103,7 @@ def test_declared_bit_exact(built, torch_cuda, nb, trunc, idle):
         _check_states(c, ob, cap)
 
 
-@pytest.mark.parametrize("nb", [20, 100, 700])
+@pytest.mark.parametrize("nb", [20, 100, 200, 700])
 def test_declared_mismatch_is_refused(built, torch_cuda, nb):
     """Bucket 2 declares group A but its ids all lie in group H (named by no
     other bucket); bucket 5 is declared idle but holds a busy entry of group
@@ -141,13 +142,14 @@ def test_declared_mismatch_is_refused(built, torch_cuda, nb):
         _check_states(c, ob, cap)                            # H, H2 states unchanged (oracle skipped them)
 
 
-@pytest.mark.parametrize("nb", [20, 700])
+@pytest.mark.parametrize("nb", [20, 100, 200, 700])
 def test_declared_mismatch_blocks_named_group_above_window(built, torch_cuda, nb):
     """A bucket declared A whose ids lie in group B, while another bucket
-    legitimately declares B.  Window launches (<= 32 buckets) refuse only the
-    disagreeing bucket; larger launches (the declared check before the crypt
-    launch) refuse both, as for two buckets naming one group (include/zrc4.h).
-    Nothing is half-crypted either way."""
+    legitimately declares B.  Launches of at most 256 buckets (the groups in
+    the kernel arguments) refuse only the disagreeing bucket; larger launches
+    (the declared check before the crypt launch) refuse both, as for two
+    buckets naming one group (include/zrc4.h).  Nothing is half-crypted
+    either way."""
     torch = torch_cuda
     rng = np.random.default_rng(1300 + nb)
     G = max(256, nb + 40)
@@ -173,8 +175,8 @@ def test_declared_mismatch_blocks_named_group_above_window(built, torch_cuda, nb
             c.sync(s)
         assert ei.value.code == -7
         got = pay.cpu().numpy()
-        # bucket 3 never runs; bucket 7 runs only on the window kernel
-        skip_entries = set(range(256 * 3, 256 * 4)) | (set() if nb <= 32 else set(range(256 * 7, 256 * 8)))
+        # bucket 3 never runs; bucket 7 runs unless the launch is checked up front
+        skip_entries = set(range(256 * 3, 256 * 4)) | (set() if nb <= 256 else set(range(256 * 7, 256 * 8)))
         keep = ids.copy()
         keep[list(skip_entries)] = IDLE_SLOT
         want = _oracle_crypt(ob, data, keep, off, L)

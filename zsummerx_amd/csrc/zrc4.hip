@@ -159,6 +159,27 @@ int launch_crypt(zrc4_ctx *c, int mode, const uint32_t *ids, uint32_t first_slot
 #undef ZRC4_WIN
         return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
     }
+    // Declared groups on the half-group / whole-group kernels (at most 256
+    // buckets, one bucket per CU): in the kernel arguments, checked there.
+    if (decl && mode == zrc4::kGrouped && !stream_kernel && grid <= zrc4::kBodyMaxBuckets) {
+        zrc4::BucketGroups dg{};
+        for (uint32_t b = 0; b < grid; ++b) dg.g[b] = decl[b];
+        const zrc4::FrameArgs fa = fr ? *fr : zrc4::FrameArgs{};
+        const bool half = ZRC4_HALF && 2u * grid <= (uint32_t)c->num_cus;
+#define ZRC4_DECL(FRAME_, HALF_, GRID_, BLK_)                                                                  \
+    hipLaunchKernelGGL((zrc4::crypt_decl_kernel<FRAME_, HALF_>), GRID_, BLK_, 0, s, c->arena, c->xy, ids, payload, \
+                       off, len, n, c->capacity, c->err, c->sink, fa, cl, dg)
+        if (half && fr)
+            ZRC4_DECL(true, true, dim3(2u * grid), dim3(zrc4::kHalfBlock));
+        else if (half)
+            ZRC4_DECL(false, true, dim3(2u * grid), dim3(zrc4::kHalfBlock));
+        else if (fr)
+            ZRC4_DECL(true, false, dim3(grid), blk);
+        else
+            ZRC4_DECL(false, false, dim3(grid), blk);
+#undef ZRC4_DECL
+        return hipGetLastError() == hipSuccess ? ZRC4_OK : ZRC4_ERR_LAUNCH;
+    }
     if (decl && mode == zrc4::kGrouped && !decl_trusted) {
         // check the declared groups before the crypt launch (stream-ordered):
         // a disagreeing bucket's groups are claimed under this launch's epoch

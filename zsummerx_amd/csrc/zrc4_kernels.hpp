@@ -924,6 +924,88 @@ __device__ __forceinline__ uint32_t image_lane_offset(uint32_t tid, bool half, u
     return half ? ((tid >> 3) << 8) | (h << 7) | ((tid & 7u) << 4) : tid << 4;
 }
 
+// A declared grouped bucket's prologue loads in one asm statement
+// (crypt_body<kGrouped, DECL>): the thread's K entries (id, length, offset),
+// its x/y, then the group's image; the entries and x/y are waited for before
+// the statement ends (vmcnt(16): only the image is younger), the image stays
+// in flight as issue_image_asm leaves it.  As compiler loads the entries and
+// x/y would be waited for with vmcnt(0) -- draining the 64 KiB image, issued
+// after them, before the bucket's table could be built.
+#define ZRC4_DECL_IMAGE                                                                          \
+    "global_load_dwordx4 v[160:163], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[164:167], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[168:171], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[172:175], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[176:179], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[180:183], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[184:187], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[188:191], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[192:195], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[196:199], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[200:203], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[204:207], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[208:211], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[212:215], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[216:219], %[vo], %[ib]\n\t"                                           \
+    "v_add_u32 %[vo], 0x1000, %[vo]\n\t"                                                         \
+    "global_load_dwordx4 v[220:223], %[vo], %[ib]\n\t"                                           \
+    "s_waitcnt vmcnt(16)\n\t"
+__device__ __forceinline__ void decl_prologue_asm1(uint32_t &id0, uint32_t &ln0, uint64_t &of0, uint32_t &xyv,
+                                                   u32x32 &ilo, u32x32 &ihi, const uint32_t *aid0,
+                                                   const uint32_t *aln0, const uint64_t *aof0, const uint16_t *axy,
+                                                   const uint8_t *ibase, uint32_t vo0)
+{
+    uint32_t vo = vo0;
+    asm volatile(
+        "global_load_dword %[id0], %[aid0], off\n\t"
+        "global_load_dword %[ln0], %[aln0], off\n\t"
+        "global_load_dwordx2 %[of0], %[aof0], off\n\t"
+        "global_load_ushort %[xyv], %[axy], off\n\t"
+        ZRC4_DECL_IMAGE
+        : [id0] "=&v"(id0), [ln0] "=&v"(ln0), [of0] "=&v"(of0), [xyv] "=&v"(xyv),
+          "=&{v[160:191]}"(ilo), "=&{v[192:223]}"(ihi), [vo] "+v"(vo)
+        : [aid0] "v"(aid0), [aln0] "v"(aln0), [aof0] "v"(aof0), [axy] "v"(axy), [ib] "s"(ibase)
+        : "memory");
+}
+__device__ __forceinline__ void decl_prologue_asm2(uint32_t &id0, uint32_t &ln0, uint64_t &of0, uint32_t &id1,
+                                                   uint32_t &ln1, uint64_t &of1, uint32_t &xyv, u32x32 &ilo,
+                                                   u32x32 &ihi, const uint32_t *aid0, const uint32_t *aln0,
+                                                   const uint64_t *aof0, const uint32_t *aid1, const uint32_t *aln1,
+                                                   const uint64_t *aof1, const uint16_t *axy, const uint8_t *ibase,
+                                                   uint32_t vo0)
+{
+    uint32_t vo = vo0;
+    asm volatile(
+        "global_load_dword %[id0], %[aid0], off\n\t"
+        "global_load_dword %[ln0], %[aln0], off\n\t"
+        "global_load_dwordx2 %[of0], %[aof0], off\n\t"
+        "global_load_dword %[id1], %[aid1], off\n\t"
+        "global_load_dword %[ln1], %[aln1], off\n\t"
+        "global_load_dwordx2 %[of1], %[aof1], off\n\t"
+        "global_load_ushort %[xyv], %[axy], off\n\t"
+        ZRC4_DECL_IMAGE
+        : [id0] "=&v"(id0), [ln0] "=&v"(ln0), [of0] "=&v"(of0), [id1] "=&v"(id1), [ln1] "=&v"(ln1),
+          [of1] "=&v"(of1), [xyv] "=&v"(xyv), "=&{v[160:191]}"(ilo), "=&{v[192:223]}"(ihi), [vo] "+v"(vo)
+        : [aid0] "v"(aid0), [aln0] "v"(aln0), [aof0] "v"(aof0), [aid1] "v"(aid1), [aln1] "v"(aln1),
+          [aof1] "v"(aof1), [axy] "v"(axy), [ib] "s"(ibase)
+        : "memory");
+}
+#undef ZRC4_DECL_IMAGE
+
 __device__ __forceinline__ void issue_image_asm(u32x32 &ilo, u32x32 &ihi, const uint8_t *ibase, uint32_t vo0)
 {
     uint32_t vo;
@@ -1166,15 +1248,26 @@ __device__ __forceinline__ void pair_meet_d(uint32_t *ctr, uint32_t &gen)
     asm volatile("" ::: "memory");
 }
 
-template <int MODE, bool FRAME, bool HALF>
+// Declared bucket groups of a grouped launch of at most 256 buckets on the
+// half-group and whole-group kernels (zrc4_crypt_grouped_declared): bucket
+// b's group, ZRC4_INVALID for a bucket with no busy entry.  By value, so it
+// sits in the kernel-argument segment (1 KiB).
+constexpr uint32_t kBodyMaxBuckets = 256;
+struct BucketGroups {
+    uint32_t g[kBodyMaxBuckets];
+};
+
+template <int MODE, bool FRAME, bool HALF, bool DECL = false>
 __device__ __forceinline__ void
 crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
            const uint32_t *__restrict__ ids, uint32_t first_slot,
            uint8_t *__restrict__ payload, const uint64_t *__restrict__ off,
            const uint32_t *__restrict__ len, uint32_t n, uint32_t capacity,
-           uint32_t *__restrict__ err, uint8_t *__restrict__ sink, const FrameArgs &fr, const Claim &cl)
+           uint32_t *__restrict__ err, uint8_t *__restrict__ sink, const FrameArgs &fr, const Claim &cl,
+           const BucketGroups *dg = nullptr)
 {
     static_assert(!HALF || MODE != kIds, "half-group workgroups run range and grouped batches");
+    static_assert(!DECL || MODE == kGrouped, "declared groups are a grouped-batch form");
     __shared__ __attribute__((aligned(16))) uint8_t smem[HALF ? kSmemHalf : kSmemDirect];
     uint8_t *S = smem;
     if (!lds_base_ok(S, err)) return;
@@ -1250,7 +1343,10 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         __syncthreads();
     }
     const uint32_t col = col_of(j);
-    volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(smem + kGroupBytes);
+    // (plain LDS words, ordered by the barriers: as `volatile` they compiled
+    // to flat stores with a vmcnt(0) after each, which drained the grouped
+    // prologue's image loads before the bucket's table was even built)
+    uint32_t *flag = reinterpret_cast<uint32_t *>(smem + kGroupBytes);
     uint4 img[16];
     u32x32 ilo, ihi;
 
@@ -1284,13 +1380,46 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         uint32_t idq[kPer], lq[kPer];
         uint64_t oq[kPer];
         bool bq[kPer];
+        // DECL: the caller's group for this bucket; its image (asm), x/y and
+        // claim leave before the entries, so the entries' round trip covers
+        // them (the entry checks below wait for the younger entries, hence
+        // for the image too: one round trip, not two)
+        uint32_t gdecl = ZRC4_INVALID;
+        uint16_t xyd = 0;
+        unsigned long long coldd = 0;
+        uint32_t rid[kPer], rln[kPer];
+        uint64_t rof[kPer];
+        if constexpr (DECL) {
+            // The entries, x/y and image in one asm statement (decl_prologue_asm*),
+            // the entries and x/y waited for inside it; an idle bucket reads
+            // group 0's image and drops it (the image registers are loaded on
+            // every path: merged with an undefined value, the compiler copied
+            // them while in flight).  The claim: thread 0, asm, waited for
+            // with the image before the fill.
+            gdecl = dg->g[w];
+            const uint32_t gl = gdecl != ZRC4_INVALID ? gdecl : 0u;
+            const uint32_t e0 = w * kGroup + tid, c0 = e0 < n ? e0 : n - 1u;
+            uint32_t xv;
+            if constexpr (kPer == 1) {
+                decl_prologue_asm1(rid[0], rln[0], rof[0], xv, ilo, ihi, ids + c0, len + c0, off + c0,
+                                   xy + gl * 256u + j, arena + (size_t)gl * kGroupBytes, vo0);
+            } else {
+                const uint32_t e1 = e0 + kLanes, c1 = e1 < n ? e1 : n - 1u;
+                decl_prologue_asm2(rid[0], rln[0], rof[0], rid[kPer - 1], rln[kPer - 1], rof[kPer - 1], xv, ilo,
+                                   ihi, ids + c0, len + c0, off + c0, ids + c1, len + c1, off + c1,
+                                   xy + gl * 256u + j, arena + (size_t)gl * kGroupBytes, vo0);
+            }
+            xyd = (uint16_t)xv;
+            if (gdecl != ZRC4_INVALID && __builtin_amdgcn_readfirstlane(tid >> 6) == 0u)
+                coldd = claim_part_async(cl, gdecl, HALF ? h : 0u, w);   // thread 0 (lane 0 of wave 0)
+        }
 #pragma unroll
         for (uint32_t q = 0; q < kPer; ++q) {
             const uint32_t eq = w * kGroup + q * kLanes + tid;
             const bool vq = eq < n;
-            uint32_t id = vq ? ids[eq] : ZRC4_INVALID;
-            lq[q] = vq ? len[eq] : 0u;
-            oq[q] = vq ? off[eq] : 0u;
+            uint32_t id = vq ? (DECL ? rid[q] : ids[eq]) : ZRC4_INVALID;
+            lq[q] = vq ? (DECL ? rln[q] : len[eq]) : 0u;
+            oq[q] = vq ? (DECL ? rof[q] : off[eq]) : 0u;
             if (vq && id >= capacity && id != ZRC4_INVALID) {   // ZRC4_IDLE_SLOT pads buckets
                 latch_fault(err, kErrSlotRange);
                 id = ZRC4_INVALID;
@@ -1304,20 +1433,29 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         // refused below) loads again once the group is known.
         bool have = false;
         uint32_t gw = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < kPer; ++q) {
-            const uint64_t bm = __ballot(bq[q]);
-            if (!have && bm) {
-                gw = __builtin_amdgcn_readlane(idq[q], (int)__builtin_ctzll(bm)) >> 8;
-                have = true;
-            }
-        }
-        issue_image_asm(ilo, ihi, arena + (size_t)gw * kGroupBytes, vo0);
-        const uint16_t xyw = xy[gw * 256u + j];
-        // the claim of this workgroup's part of the group (Claim), by thread 0
-        // on its wave's guess; re-issued below if that wave had no busy entry
+        uint16_t xyw = 0;
         unsigned long long cold = 0;
-        if (tid == 0 && have) cold = claim_part(cl, gw, HALF ? h : 0u, w);
+        if constexpr (DECL) {
+            have = gdecl != ZRC4_INVALID;
+            gw = have ? gdecl : 0u;
+            xyw = xyd;
+            cold = coldd;
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < kPer; ++q) {
+                const uint64_t bm = __ballot(bq[q]);
+                if (!have && bm) {
+                    gw = __builtin_amdgcn_readlane(idq[q], (int)__builtin_ctzll(bm)) >> 8;
+                    have = true;
+                }
+            }
+            issue_image_asm(ilo, ihi, arena + (size_t)gw * kGroupBytes, vo0);
+            xyw = xy[gw * 256u + j];
+            // the claim of this workgroup's part of the group (Claim), by
+            // thread 0 on its wave's guess; re-issued below if that wave had
+            // no busy entry
+            if (tid == 0 && have) cold = claim_part(cl, gw, HALF ? h : 0u, w);
+        }
 #pragma unroll
         for (uint32_t q = 0; q < kPer; ++q) te[q * kLanes + tid] = ZRC4_INVALID;
         if (tid == 0) {
@@ -1328,13 +1466,14 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         }
         __syncthreads();
         if (have && (tid & 63u) == 0u) {
-            atomicMin(const_cast<uint32_t *>(flag), gw);
-            atomicMax(const_cast<uint32_t *>(flag + 1), gw);
+            atomicMin(flag, gw);
+            atomicMax(flag + 1, gw);
         }
 #pragma unroll
         for (uint32_t q = 0; q < kPer; ++q) {
             if (bq[q]) {
                 const uint32_t k = idq[q] & 255u;
+                if (DECL && !have) flag[2] = 1u;                                          // declared idle, yet busy
                 if ((idq[q] >> 8) != gw) flag[2] = 1u;                                  // another group
                 if (atomicExch(&te[k], w * kGroup + q * kLanes + tid) != ZRC4_INVALID) flag[2] = 1u;   // a slot twice
                 tl[k] = lq[q];
@@ -1345,7 +1484,9 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         __syncthreads();
         const uint32_t gmin = flag[0], gmax = flag[1], dup = flag[2];
         if (gmin == 0xFFFFFFFFu || gmin != gmax || dup) {
-            if (gmin != 0xFFFFFFFFu && tid == 0) latch_fault(err, kErrGroup);
+            if ((gmin != 0xFFFFFFFFu || dup) && tid == 0) latch_fault(err, kErrGroup);
+            if constexpr (DECL)                          // (no load left in flight at exit)
+                asm volatile("s_waitcnt vmcnt(0)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
             if constexpr (FRAME) {                       // an idle bucket still reports its framing
                 if (valid && gmin == 0xFFFFFFFFu)
                     frame_walk(payload + fr.off[e], fr.len[e], fr.bound, fr.maxp, e, fr.npk, fr.used, fr.status,
@@ -1360,12 +1501,13 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         myoff = ent != ZRC4_INVALID ? to[j] : 0u;
         slot = g * 256u + j;
         sxy = xyw;
-        if (!have || gw != g) {                          // wave-uniform: the guess missed
+        if (!DECL && (!have || gw != g)) {               // wave-uniform: the guess missed
             asm volatile("s_waitcnt vmcnt(0)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
             issue_image_asm(ilo, ihi, arena + (size_t)g * kGroupBytes, vo0);
             sxy = xy[slot];
         }
-        if (tid == 0 && !have) cold = claim_part(cl, g, HALF ? h : 0u, w);
+        if (!DECL && tid == 0 && !have) cold = claim_part(cl, g, HALF ? h : 0u, w);
+        if constexpr (DECL) claim_wait(cold);            // (the image too: it is needed by the fill next)
         if (tid == 0) flag[3] = claim_lost(cl, cold) ? 1u : 0u;          // read after the fill barrier
         if (!mylen) sxy = 0;
         if constexpr (FRAME) {
@@ -1482,6 +1624,20 @@ crypt_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
              Claim cl = Claim{})
 {
     crypt_body<MODE, FRAME, false>(arena, xy, ids, first_slot, payload, off, len, n, capacity, err, sink, fr, cl);
+}
+
+// The grouped forms with declared bucket groups (zrc4_crypt_grouped_declared,
+// 33..256 buckets): the groups in the kernel arguments.
+template <bool FRAME, bool HALF>
+__global__ void __launch_bounds__(HALF ? (ZRC4_HALF_PAD ? 256u : 128u) : 256u, HALF ? 1 : 2)
+crypt_decl_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
+                  const uint32_t *__restrict__ ids, uint8_t *__restrict__ payload,
+                  const uint64_t *__restrict__ off, const uint32_t *__restrict__ len, uint32_t n,
+                  uint32_t capacity, uint32_t *__restrict__ err, uint8_t *__restrict__ sink, FrameArgs fr,
+                  Claim cl, BucketGroups dg)
+{
+    crypt_body<kGrouped, FRAME, HALF, true>(arena, xy, ids, 0u, payload, off, len, n, capacity, err, sink, fr, cl,
+                                            &dg);
 }
 
 // Half-group workgroups (kRange / kGrouped, few groups): one per CU;

@@ -377,24 +377,26 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
     uint8_t *img = arena + (size_t)(slot >> 8) * kGroupBytes + 4u * q;
     uint8_t *msg = payload + O;
     const bool aligned = ((uintptr_t)msg & 15u) == 0u;
-    uint8_t *S = Sb + b * 256u;
-    uint32_t *M = Mk + b * 256u;
-    uint8_t *R = Ring + b * kWinRing;
-    // the S-boxes into LDS (the wave's 4 streams share every dword of the
-    // image column) and the markers cleared
-    auto fill = [&]() {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t kk = lane + 64u * r;
-#pragma unroll
-            for (uint32_t s4 = 0; s4 < 4; ++s4) {
-                const uint8_t v = (uint8_t)(rows[r] >> (8 * s4));
-                Sb[s4 * 256u + kk] = v;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) reinterpret_cast<uint4 *>(Mk)[lane + 64 * i] = make_uint4(0, 0, 0, 0);
-    };
+
+    // The S-boxes into LDS (the wave's 4 streams share every dword of the
+    // image column) and the markers cleared.  kGrouped: before the payload
+    // prefetch, whose addresses come from the slot table (a second round
+    // trip): with the prefetch issued first, the compiler's wait for the
+    // image column (older, on a path the per-lane prefetch branches join)
+    // drained the prefetch too, a round trip on the way to the first window
+    // (r05 timeline: prologue 3.84 vs 2.24 us range, profiles/r05/tl1/).
+#define ZRC4_WIN_FILL                                                                       \
+    do {                                                                                    \
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                     \
+            const uint32_t kk = lane + 64u * r;                                             \
+            _Pragma("unroll") for (uint32_t s4 = 0; s4 < 4; ++s4) {                         \
+                const uint8_t v = (uint8_t)(rows[r] >> (8 * s4));                           \
+                Sb[s4 * 256u + kk] = v;                                                     \
+            }                                                                               \
+        }                                                                                   \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                       \
+            reinterpret_cast<uint4 *>(Mk)[lane + 64 * i] = make_uint4(0, 0, 0, 0);         \
+    } while (0)
     if constexpr (MODE == kGrouped) {
         if (bad) {
             claim_wait(cold);                                                 // (no load left in flight at exit)
@@ -406,13 +408,7 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
             claim_wait(cold);
             return;
         }
-        // The fill goes before the payload prefetch here: its addresses come
-        // from the slot table (a second round trip), and with the prefetch
-        // issued first the compiler's wait for the image column (older, on
-        // a path the per-lane prefetch branches join) drained the prefetch
-        // too, a round trip on the way to the first window (r05 timeline:
-        // prologue 3.84 vs 2.24 us range, profiles/r05/tl1/).
-        fill();
+        ZRC4_WIN_FILL;
     }
 
     // payload prefetch of chunk 0 (aligned messages: whole 16-byte units).
@@ -425,14 +421,18 @@ crypt_win_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy, const u
 #pragma unroll
     for (uint32_t u = 0; u < kWinUnits; ++u) {
         const uint32_t pos = 16u * (l + kWinLanes * u);
-        const bool use = aligned && pos + 16u <= L;
         if constexpr (MODE == kGrouped)
-            pre[u] = *reinterpret_cast<const uint4 *>(use ? msg + pos : sink + 16u * lane);
-        else if (use)
+            pre[u] = *reinterpret_cast<const uint4 *>(aligned && pos + 16u <= L ? msg + pos : sink + 16u * lane);
+        else if (aligned && pos + 16u <= L)
             pre[u] = *reinterpret_cast<const uint4 *>(msg + pos);
     }
     if constexpr (MODE == kGrouped) cold = claim_part_async(cl, gclaim, q, wg);
-    if constexpr (MODE != kGrouped) fill();
+
+    uint8_t *S = Sb + b * 256u;
+    uint32_t *M = Mk + b * 256u;
+    uint8_t *R = Ring + b * kWinRing;
+    if constexpr (MODE != kGrouped) ZRC4_WIN_FILL;
+#undef ZRC4_WIN_FILL
     __syncthreads();                                 // (grouped: also the tables read before the ring is used)
     stamp(ts, 1);
 

@@ -132,6 +132,19 @@ struct Table {
     }
 };
 
+// A grouped launch over table t: the groups built here are declared with it
+// up to 256 buckets, where the kernels take them in their arguments and load
+// each bucket's state with its entries; above that the persistent kernel
+// prefetches every bucket's ids a bucket ahead anyway, and a declaration
+// would only add the library's up-front check (include/zrc4.h).
+int launchGrouped(zrc4_ctx *ctx, const Table &t, uint8_t *base, const zrc4_frame_args *fa, hipStream_t s)
+{
+    if (t.groups.size() <= 256u)
+        return zrc4_crypt_grouped_declared(ctx, t.ids.p, t.groups.data(), base, t.off.p, t.len.p, t.n, fa, s);
+    return fa ? zrc4_crypt_grouped_frame(ctx, t.ids.p, base, t.off.p, t.len.p, t.n, fa, s)
+              : zrc4_crypt_grouped(ctx, t.ids.p, base, t.off.p, t.len.p, t.n, s);
+}
+
 struct Entry {
     uint32_t slot;
     uint32_t len;
@@ -417,8 +430,7 @@ public:
         buildGrouped(tt_, es_, &ft_);
         zrc4_frame_args fa{ft_.off.p, ft_.len.p, bound, Rc4Frame::kMaxPackets, ft_.npk.p, ft_.used.p,
                            ft_.status.p, ft_.pkt.p};
-        rc = zrc4_crypt_grouped_declared(ctx_, tt_.ids.p, tt_.groups.data(), base_, tt_.off.p, tt_.len.p, tt_.n,
-                                         &fa, sA_);
+        rc = launchGrouped(ctx_, tt_, base_, &fa, sA_);
         if (rc != ZRC4_OK) return rc;
         ++tailLaunches_;
         if ((rc = zrc4_sync(ctx_, sA_)) != ZRC4_OK) return rc;
@@ -476,8 +488,7 @@ private:
     {
         if (es.empty()) return ZRC4_OK;
         buildGrouped(tt_, es);
-        int rc = zrc4_crypt_grouped_declared(ctx_, tt_.ids.p, tt_.groups.data(), base_, tt_.off.p, tt_.len.p, tt_.n,
-                                             nullptr, sA_);
+        int rc = launchGrouped(ctx_, tt_, base_, nullptr, sA_);
         if (rc != ZRC4_OK) return rc;
         ++tailLaunches_;
         return zrc4_sync(ctx_, sA_);
@@ -616,8 +627,7 @@ private:
         hungry_.swap(keep);
         if (rs_.empty()) return ZRC4_OK;
         buildGrouped(R.t, rs_);
-        int rc = zrc4_crypt_grouped_declared(ctx_, R.t.ids.p, R.t.groups.data(), base_, R.t.off.p, R.t.len.p,
-                                             R.t.n, nullptr, sB_);
+        int rc = launchGrouped(ctx_, R.t, base_, nullptr, sB_);
         if (rc != ZRC4_OK) {
             // nothing queued: the levels go back (pend > gen with no refill in
             // flight would make cryptReservoir wait for bytes that never come)
