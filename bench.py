@@ -396,6 +396,8 @@ def kernel_name(S: int, ids: str = "range") -> str:
         return "zrc4::crypt_stream_kernel<false, false, false>" if groups > cus else "zrc4::crypt_kernel<0, false>"
     if groups <= WIN_MAX_GROUPS:
         return f"zrc4::crypt_win_kernel<{mode}, false, {'true' if ids == 'declared' else 'false'}>"
+    if ids == "declared" and groups <= 256:
+        return f"zrc4::crypt_decl_kernel<false, {'true' if 2 * groups <= cus else 'false'}>"
     if 2 * groups <= cus:
         return f"zrc4::crypt_half_kernel<{mode}, false>"
     if groups <= cus:

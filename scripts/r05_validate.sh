@@ -22,12 +22,14 @@ fi
 step bench_default 300 python bench.py --steps 20 --warmup 5
 step bench_default_200 300 python bench.py --steps 200 --warmup 20 --cpu-seconds 0
 step bench_cfg2_grouped 300 python bench.py --ids grouped --steps 200 --warmup 20 --cpu-seconds 0 --companion-workload none
+step bench_cfg2_declared 300 python bench.py --ids declared --steps 200 --warmup 20 --cpu-seconds 0 --companion-workload none
 step bench_cfg5 300 python bench.py --workload cfg5 --steps 200 --warmup 120 --cpu-seconds 0
 step bench_cfg5_grouped 300 python bench.py --workload cfg5 --ids grouped --steps 200 --warmup 120 --cpu-seconds 0
 step bench_cfg3 200 python bench.py --workload cfg3 --steps 200 --warmup 20 --cpu-seconds 0
+step bench_cfg3_declared 200 python bench.py --workload cfg3 --ids declared --steps 200 --warmup 20 --cpu-seconds 0
 step bench_cfg4 200 python bench.py --workload cfg4 --steps 50 --warmup 5 --cpu-seconds 0
 cd /tmp && export TMPDIR=/tmp
-for wl in cfg2 cfg3 cfg4 cfg5 cfg5-grouped cfg2-grouped; do
+for wl in cfg2 cfg3 cfg4 cfg5 cfg5-grouped cfg2-grouped cfg2-declared cfg3-declared; do
   W=20; [ ${wl%%-*} = cfg5 ] && W=120
   IDS=range; [ "${wl#*-}" != "$wl" ] && IDS=${wl#*-}
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $ROOT/$OUT/prof_$wl -o run --output-format csv \
@@ -36,5 +38,5 @@ for wl in cfg2 cfg3 cfg4 cfg5 cfg5-grouped cfg2-grouped; do
   rc=$?; echo "[rocprof $wl] rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 cd $ROOT
-bash scripts/pmc_traffic.sh ${VAL_PMC:-cfg2 cfg5 cfg5-grouped cfg2-grouped cfg3 cfg4} || exit $?
+bash scripts/pmc_traffic.sh ${VAL_PMC:-cfg2 cfg5 cfg5-grouped cfg2-grouped cfg2-declared cfg3 cfg3-declared cfg4} || exit $?
 echo validate done
