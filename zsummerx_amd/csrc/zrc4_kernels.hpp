@@ -1220,11 +1220,19 @@ constexpr uint32_t kSmemDirect = kSidOff + 16;                // 69 664 B: two w
 constexpr uint32_t kSmemHalf = 96 * 1024;                     // one workgroup per CU
 
 // Workgroup k runs on XCD k mod 8.  xcd_run_map deals the groups so that
-// each XCD takes runs of 8 consecutive groups per 64: k = 64s + 8r + x ->
-// 64s + 8x + r (bijective; a tail of grid mod 64 groups keeps its order).
+// each XCD takes runs of R = ZRC4_XCD_RUN consecutive groups per 8R: k =
+// 8R s + 8 r + x -> 8R s + R x + r (bijective; a tail of grid mod 8R groups
+// keeps its order; R = 1 is the identity).
+#ifndef ZRC4_XCD_RUN
+#define ZRC4_XCD_RUN 8
+#endif
+static_assert(ZRC4_XCD_RUN >= 1 && ZRC4_XCD_RUN <= 32 && (ZRC4_XCD_RUN & (ZRC4_XCD_RUN - 1)) == 0,
+              "XCD run length: a power of two");
 __device__ __forceinline__ uint32_t xcd_run_map(uint32_t k, uint32_t grid)
 {
-    return k >= (grid & ~63u) ? k : (k & ~63u) | ((k & 7u) << 3) | ((k >> 3) & 7u);
+    constexpr uint32_t R = ZRC4_XCD_RUN, B = 8u * R;
+    if (k >= (grid & ~(B - 1u))) return k;
+    return (k & ~(B - 1u)) | ((k & 7u) * R) | ((k >> 3) & (R - 1u));
 }
 
 // ZRC4_PAIR_DIRECT: whole-group range launches (crypt_kernel<kRange>) by
