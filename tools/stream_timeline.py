@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
 """Where a crypt_stream_kernel launch spends its time (diagnostic build).
 
-Builds libzrc4 with ZRC4_TIMING=1: lane 0 of every workgroup's first wave
-stamps s_memrealtime (100 MHz) at kernel entry, at the start and end of each
-group's keystream, and at exit (zrc4_kernels.hpp, stream_stamp).  The last of
---launches back-to-back launches is read back and summarised per workgroup:
+Builds libzrc4 with ZRC4_TIMING=1: lane 0 of the first wave of every wave
+pair (waves 0 and 2 of each workgroup) stamps s_memrealtime (100 MHz) at
+kernel entry, at the start and end of each group's keystream, and at exit
+(zrc4_kernels.hpp, stream_stamp).  The last of --launches back-to-back
+launches is read back and summarised per workgroup (its pair 0, as the
+pre-r05 timelines) and per pair:
 
   prologue   first keystream start - entry   (first image + entries + lines)
   chain k    keystream of the k-th group walked (all its messages)
   boundary k start of group k+1 - end of group k (image out, next image in, barriers)
   epilogue   exit - end of the last group (last image store, drained)
+
+and "what_if" replays each pair's own sequence with one component replaced
+(every prologue the launch's fastest / median one, every chain the median of
+its group index, no boundaries) to bound what removing that component's
+spread could give the launch span.
 
   python tools/stream_timeline.py --workloads cfg5,131072x1024
 """
@@ -95,6 +102,48 @@ def by_place(rt: np.ndarray, hwid: np.ndarray, wgs: int, K: int) -> dict:
     return out
 
 
+def what_if(rt: np.ndarray, rows: int, K: int) -> dict:
+    """Launch span (us) if each pair ran its own recorded sequence with one
+    component replaced.  Pair p: entry e, prologue P, chains C_k, boundaries
+    B_k, epilogue E; end = e + P + sum C + sum B + E (exactly its exit)."""
+    r = rt[:rows].astype(np.float64) * 10.0 / 1000.0
+    e = r[:, 0]
+    t0 = e.min()
+    P = r[:, 1] - r[:, 0]
+    C = np.stack([r[:, 2 + 2 * k] - r[:, 1 + 2 * k] for k in range(K)], axis=1)
+    B = np.stack([r[:, 3 + 2 * k] - r[:, 2 + 2 * k] for k in range(K - 1)], axis=1) if K > 1 else np.zeros((rows, 0))
+    E = r[:, 15] - r[:, 2 + 2 * (K - 1)]
+
+    def span(e_, P_, C_, B_, E_):
+        return round(float((e_ + P_ + C_.sum(1) + B_.sum(1) + E_).max() - t0), 2)
+
+    end = e + P + C.sum(1) + B.sum(1) + E
+    out = {"recorded": span(e, P, C, B, E),
+           "prologue_fastest": span(e, np.full_like(P, P.min()), C, B, E),
+           "prologue_median": span(e, np.minimum(P, np.median(P)), C, B, E),
+           "no_entry_skew": span(np.full_like(e, t0), P, C, B, E),
+           "chains_median": span(e, P, np.broadcast_to(np.median(C, 0), C.shape), B, E),
+           "chains_fastest_quartile": span(e, P, np.minimum(C, np.percentile(C, 25, axis=0)), B, E),
+           "no_boundaries": span(e, P, C, np.zeros_like(B), E),
+           "prologue_median_and_chains_median": span(e, np.minimum(P, np.median(P)),
+                                                     np.broadcast_to(np.median(C, 0), C.shape), B, E),
+           "sum_chain_median": round(float(np.median(C.sum(1))), 2)}
+    # which component the 16 latest pairs lose their time in, against the median pair
+    late = np.argsort(end)[-16:]
+    med = {"entry": np.median(e - t0), "prologue": np.median(P), "chains": np.median(C.sum(1)),
+           "boundaries": np.median(B.sum(1)), "epilogue": np.median(E)}
+    out["latest16_excess_over_median"] = {
+        "entry": round(float(np.mean(e[late] - t0) - med["entry"]), 2),
+        "prologue": round(float(np.mean(P[late]) - med["prologue"]), 2),
+        "chains": round(float(np.mean(C[late].sum(1)) - med["chains"]), 2),
+        "boundaries": round(float(np.mean(B[late].sum(1)) - med["boundaries"]), 2),
+        "epilogue": round(float(np.mean(E[late]) - med["epilogue"]), 2)}
+    out["corr_end_with"] = {n: round(float(np.corrcoef(end, v)[0, 1]), 3)
+                            for n, v in (("entry", e), ("prologue", P), ("chains", C.sum(1)),
+                                         ("boundaries", B.sum(1)))}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workloads", default="cfg5,131072x1024")
@@ -171,22 +220,29 @@ def main():
         last_event_us = ev0.elapsed_time(ev1) * 1000.0
         sink = C.c_void_p()
         _capi.check(lib.zrc4_debug_sink(h, C.byref(sink)))
-        rt = np.zeros((512, 16), dtype=np.uint64)
-        clk = np.zeros((512, 2), dtype=np.uint64)
-        hwid = np.zeros((512, 2), dtype=np.uint32)
-        for arr, o in ((rt, 0), (clk, 65536), (hwid, 65536 + 8192)):
+        rt = np.zeros((1024, 16), dtype=np.uint64)     # record 2 wg + pair
+        clk = np.zeros((1024, 2), dtype=np.uint64)
+        hwid = np.zeros((1024, 2), dtype=np.uint32)
+        base = 65536 + 16384                            # zrc4_kernels.hpp kStampBase
+        for arr, o in ((rt, base), (clk, base + 131072), (hwid, base + 131072 + 16384)):
             rc = hip.hipMemcpy(C.c_void_p(arr.ctypes.data), C.c_void_p(sink.value + o), C.c_size_t(arr.nbytes), 2)
             if rc:
                 raise SystemExit(f"hipMemcpy failed {rc}")
         groups = -(-S // 256)
         wgs = min(groups, 512)
-        out[wl] = summarise(rt, clk, wgs, min(7, groups // wgs))
+        K = min(7, groups // wgs)
+        wrt, wclk, whw = rt[0::2], clk[0::2], hwid[0::2]        # pair 0 of each workgroup
+        out[wl] = summarise(wrt, wclk, wgs, K)
         out[wl]["ids"] = args.ids
         out[wl]["last_launch_event_us"] = round(last_event_us, 2)
-        out[wl]["by_place"] = by_place(rt, hwid, wgs, min(7, groups // wgs))
+        out[wl]["by_place"] = by_place(wrt, whw, wgs, K)
+        out[wl]["pairs"] = summarise(rt, clk, 2 * wgs, K)
+        out[wl]["pairs"]["partner_end_diff_us"] = q(np.abs(rt[0:2 * wgs:2, 15].astype(np.float64) -
+                                                           rt[1:2 * wgs:2, 15].astype(np.float64)) / 100.0)
+        out[wl]["pairs"]["what_if"] = what_if(rt, 2 * wgs, K)
         print(wl, json.dumps(out[wl]), flush=True)
         if args.dump:
-            np.savez(f"{args.dump}_{wl}.npz", rt=rt[:wgs], clk=clk[:wgs], hwid=hwid[:wgs])
+            np.savez(f"{args.dump}_{wl}.npz", rt=rt[:2 * wgs], clk=clk[:2 * wgs], hwid=hwid[:2 * wgs])
         lib.zrc4_destroy(h)
         del keys, pay, off, ln, klen, koff
         torch.cuda.empty_cache()

@@ -162,22 +162,28 @@ __device__ __forceinline__ void stamp(Stamps &s, int i)
     s.c[i] = __builtin_amdgcn_s_memtime();
 #endif
 }
-// crypt_stream_kernel (ZRC4_TIMING): lane 0 of workgroup wg's wave 0 stamps
-// event i (0 entry, 1 + 2k / 2 + 2k group k's keystream start / end, 15 exit)
-// as s_memrealtime into sink[wg * 16 + i] (512 workgroups); entry and exit
-// shader clocks go to sink + 64 KiB, HW_ID / XCC_ID to sink + 72 KiB.
+// crypt_stream_kernel (ZRC4_TIMING): lane 0 of the first wave of each wave
+// pair (waves 0 and 2) of workgroup wg stamps event i (0 entry, 1 + 2k / 2 +
+// 2k group k's keystream start / end, 15 exit; 9-13 inside boundary 0) as
+// s_memrealtime into record r = 2 wg + pair (512 workgroups, 1 024 pairs) of
+// the stamp area after the crypt_kernel records: rt[r][16] at kStampBase,
+// entry / exit shader clocks at + 128 KiB, HW_ID / XCC_ID at + 144 KiB.
+constexpr uint32_t kStampBase = 65536u + 16384u;
+constexpr uint32_t kStampBytes = 131072u + 16384u + 8192u;
 __device__ __forceinline__ void stream_stamp(uint8_t *sink, uint32_t i)
 {
 #if ZRC4_TIMING
-    if (threadIdx.x == 0u && blockIdx.x < 512u && i < 16u) {
-        reinterpret_cast<uint64_t *>(sink)[blockIdx.x * 16u + i] = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 127u) == 0u && blockIdx.x < 512u && i < 16u) {
+        const uint32_t r = blockIdx.x * 2u + (threadIdx.x >> 7);
+        uint8_t *b = sink + kStampBase;
+        reinterpret_cast<uint64_t *>(b)[r * 16u + i] = __builtin_amdgcn_s_memrealtime();
         if (i == 0u || i == 15u)
-            reinterpret_cast<uint64_t *>(sink + 65536u)[blockIdx.x * 2u + (i ? 1u : 0u)] = __builtin_amdgcn_s_memtime();
+            reinterpret_cast<uint64_t *>(b + 131072u)[r * 2u + (i ? 1u : 0u)] = __builtin_amdgcn_s_memtime();
         if (i == 0u) {
             uint32_t hw, xcc;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
                          : "=s"(hw), "=s"(xcc));
-            uint32_t *o = reinterpret_cast<uint32_t *>(sink + 65536u + 8192u) + blockIdx.x * 2u;
+            uint32_t *o = reinterpret_cast<uint32_t *>(b + 131072u + 16384u) + r * 2u;
             o[0] = hw;
             o[1] = xcc;
         }
@@ -607,7 +613,7 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr uint32_t kSinkSlot = 256;                 // bytes of sink per thread (128-B line + offsets)
 constexpr uint32_t kSinkBytes = kGroup * kSinkSlot  // one 64 KiB sink per context, shared by all workgroups
-                                + (ZRC4_TIMING ? 16384u : 0u);  // + where each timed wave ran / stream clocks and ids
+                                + (ZRC4_TIMING ? 16384u + kStampBytes : 0u);  // + where each timed wave ran, stream stamps
 
 // line = blocks at b0 (16 B x 4) and b1 (16 B x 4)
 __device__ __forceinline__ void preload_line(u32x32 &v, const uint8_t *b0, const uint8_t *b1)
@@ -2373,7 +2379,17 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
     } else {
         load_entry(cur, w, j, ids, first_slot, off, len, n, capacity, err, xy);
     }
-    if constexpr (PF && !GR) load_image((first_slot >> 8) + w);
+#ifndef ZRC4_AB_NOIMG0
+#define ZRC4_AB_NOIMG0 0     // timing-only ablation: the first group's image is never loaded (outputs wrong)
+#endif
+    if constexpr (PF && !GR) {
+        if constexpr (ZRC4_AB_NOIMG0) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) ilo[i] = ihi[i] = 0u;
+        } else {
+            load_image((first_slot >> 8) + w);
+        }
+    }
     LineSetup ls;
     line_setup(ls, payload + cur.off, cur.len);
     u32x32 P, Q = {};
