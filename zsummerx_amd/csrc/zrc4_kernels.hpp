@@ -1810,8 +1810,12 @@ constexpr uint32_t kSmemStreamGr = kGroupBytes + 4u * (kGrTab + 256u);   // 66 6
 // The table of bucket nb from its raw entries (thread j holds entry nb*256 +
 // j), plus this wave's vote.  Call between two barriers that order it after
 // every read of the previous table.
+// lo (ZRC4_GR_FASTPRO prologue): each busy entry also leaves its length at
+// lo[slot & 255] and its offset at lo + 256 (u64) -- the permuted entry the
+// lane of that column would otherwise gather from HBM.
 __device__ __forceinline__ void bucket_table(uint32_t *gr, uint32_t nb, uint32_t id, uint32_t ln, uint32_t n,
-                                             uint32_t capacity, uint32_t *err)
+                                             uint32_t capacity, uint32_t *err, uint32_t *lo = nullptr,
+                                             uint64_t of = 0)
 {
     const uint32_t j = threadIdx.x, e = nb * kGroup + j;
     const bool v = e < n;
@@ -1823,6 +1827,10 @@ __device__ __forceinline__ void bucket_table(uint32_t *gr, uint32_t nb, uint32_t
     const uint64_t bm = __ballot(busy);
     const uint32_t guess = bm ? __builtin_amdgcn_readlane(id, (int)__builtin_ctzll(bm)) >> 8 : ZRC4_INVALID;
     const uint32_t old = busy ? atomicExch(&gr[kGrTab + (id & 255u)], e) : ZRC4_INVALID;
+    if (lo && busy) {                        // (a slot named twice refuses the bucket: its values are unused)
+        lo[id & 255u] = ln;
+        reinterpret_cast<uint64_t *>(lo + 256u)[id & 255u] = of;
+    }
     const bool bad = __ballot(busy && ((id >> 8) != guess || (old >> 8) == nb)) != 0u;
     if ((j & 63u) == 0u) {
         const uint32_t wv = __builtin_amdgcn_readfirstlane(j >> 6);   // (an SGPR: no VGPR held across the loop)
@@ -1883,7 +1891,13 @@ constexpr uint32_t kGrPairWords = kGrPairCnt + 512u;      // votes, lost, table,
 constexpr uint32_t kGrMeet = 2u * kGrPairWords;           // 2 pair-meet counters
 constexpr uint32_t kGrCnt = kGrMeet + 2u;                 // 2 boundaries-done counters
 constexpr uint32_t kGrStg = kGrCnt + 2u;                  // 2 x 256 raw entries {id, len}
-constexpr uint32_t kSmemStreamGrPair = kGroupBytes + 4u * (kGrStg + 1024u);   // 75 920 B: two workgroups per CU
+// ZRC4_GR_FASTPRO: the first bucket's permuted lengths (256 words) and
+// offsets (256 u64), written with its table in the prologue
+#ifndef ZRC4_GR_FASTPRO
+#define ZRC4_GR_FASTPRO 1
+#endif
+constexpr uint32_t kGrPro = kGrStg + 1024u;
+constexpr uint32_t kSmemStreamGrPair = kGroupBytes + 4u * (kGrPro + (ZRC4_GR_FASTPRO ? 768u : 0u));   // 78 992 B: two workgroups per CU
 
 // Pair version of the bucket table, in two halves around the pair's meet
 // so that a boundary pays two LDS round trips (each one queues behind the
@@ -2204,6 +2218,8 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             }
         }
     };
+    LineSetup ls;
+    u32x32 P, Q = {};
     // GR: this bucket's group and whether it runs (wave-uniform), its claim
     // word's old value (lane 0 of wave 0), and the next bucket's raw entry.
     uint32_t gcur = 0;
@@ -2236,15 +2252,32 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         pre = ZRC4_GR_PRECLAIM && KB >= 3u;
         const uint32_t wv = __builtin_amdgcn_readfirstlane(j >> 6);
         uint32_t idk[8], lk[8];
+        // (unconditional loads from a clamped entry, selected afterwards: a
+        // load under a lane mask is merged with its default before the next
+        // one is issued, i.e. one round trip per bucket)
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const uint32_t e = (w + m * gridDim.x) * kGroup + j;
+            const uint32_t ec = e < n ? e : n - 1u;
+            idk[m] = ids[ec];
+            lk[m] = len[ec];
+        }
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
             const uint32_t e = (w + m * gridDim.x) * kGroup + j;
             const bool v = (uint32_t)m < KB && e < n;
-            idk[m] = v ? ids[e] : ZRC4_INVALID;
-            lk[m] = v ? len[e] : 0u;
+            idk[m] = v ? idk[m] : ZRC4_INVALID;
+            lk[m] = v ? lk[m] : 0u;
         }
         qid = idk[2];
         qlen = lk[2];
+#if ZRC4_GR_FASTPRO
+        // Bucket 0's offsets with its ids: its table hands each column its
+        // length and offset through LDS, so line 0 needs no gather round trip
+        // (the image itself waits for the table: issued before the claims, its
+        // loads would be drained by the wait for the claims' answers)
+        const uint64_t of0 = off[w * kGroup + j < n ? w * kGroup + j : n - 1u];   // (unused past n)
+#endif
         *reinterpret_cast<uint2 *>(gr + kGrStg + 512u + 2u * j) = make_uint2(idk[1], lk[1]);
 #if ZRC4_GR_PRECLAIM
         // Claims up front: each of this workgroup's first 64 buckets whose
@@ -2297,7 +2330,11 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         if (pre) votes(idk, lk);
 #endif
         __syncthreads();
+#if ZRC4_GR_FASTPRO
+        bucket_table(gr, w, idk[0], lk[0], n, capacity, err, gr + kGrPro, of0);
+#else
         bucket_table(gr, w, idk[0], lk[0], n, capacity, err);
+#endif
 #if ZRC4_GR_PRECLAIM
         if (pre) mixed(idk, lk);
 #endif
@@ -2307,7 +2344,7 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         cur_ok = bv.ok;
 #if ZRC4_GR_PRECLAIM
         // (batch 0's answers are collected after the image loads are issued)
-        const uint32_t old0 = pre ? claim(0u) : 0u;
+        uint32_t old0 = pre ? claim(0u) : 0u;
         if (!pre && bv.ok && (j & 127u) == 0u)
             cold = __hip_atomic_exchange(reinterpret_cast<uint32_t *>(cl.word + (size_t)bv.g * kClaimParts + pr) + 1,
                                          cl.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2320,9 +2357,16 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
 #pragma unroll
                 for (int m = 0; m < 8; ++m) {
                     const uint32_t e = (w + (k0 + m) * gridDim.x) * kGroup + j;
+                    const uint32_t ec = e < n ? e : n - 1u;
+                    ik[m] = ids[ec];
+                    lkk[m] = len[ec];
+                }
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    const uint32_t e = (w + (k0 + m) * gridDim.x) * kGroup + j;
                     const bool v = k0 + m < K && e < n;
-                    ik[m] = v ? ids[e] : ZRC4_INVALID;
-                    lkk[m] = v ? len[e] : 0u;
+                    ik[m] = v ? ik[m] : ZRC4_INVALID;
+                    lkk[m] = v ? lkk[m] : 0u;
                 }
                 __syncthreads();                         // the previous round's scratch is read
                 votes(ik, lkk);
@@ -2339,11 +2383,26 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             cold = __hip_atomic_exchange(reinterpret_cast<uint32_t *>(cl.word + (size_t)bv.g * kClaimParts + (j >> 7)) + 1,
                                          cl.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
+#if ZRC4_GR_FASTPRO
+        cur.len = bv.valid ? gr[kGrPro + j] : 0u;
+        cur.off = bv.valid ? reinterpret_cast<const uint64_t *>(gr + kGrPro + 256u)[j] : 0u;
+        cur.slot = bv.valid ? bv.g * 256u + j : ZRC4_INVALID;
+        cur.xy = xy[bv.g * 256u + j];
+        load_image(gcur);
+        // line 0 now, behind the claims and the image, before their answers
+        // are waited for below
+        line_setup(ls, payload + cur.off, cur.len);
+        preload_line0(P, ls, sk);
+        // the claims' answers after these loads: compared earlier, the wait
+        // for them would drain the loads issued behind them
+        asm volatile("" : "+v"(old0) :: "memory");
+#else
         cur.len = bv.valid ? len[bv.ent] : 0u;
         cur.off = bv.valid ? off[bv.ent] : 0u;
         cur.slot = bv.valid ? bv.g * 256u + j : ZRC4_INVALID;
         cur.xy = xy[bv.g * 256u + j];
         load_image(gcur);                     // with the entry gathers, not after the barrier
+#endif
 #if ZRC4_GR_PRECLAIM
         if (pre && K <= 8u) lost_to_lds(old0);
 #endif
@@ -2390,10 +2449,10 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             load_image((first_slot >> 8) + w);
         }
     }
-    LineSetup ls;
-    line_setup(ls, payload + cur.off, cur.len);
-    u32x32 P, Q = {};
-    preload_line0(P, ls, sk);
+    if constexpr (!PG || !ZRC4_GR_FASTPRO) {
+        line_setup(ls, payload + cur.off, cur.len);
+        preload_line0(P, ls, sk);
+    }
     // Retire the prologue's loads here, once: inside the loop the compiler's
     // waitcnt analysis merges the first iteration with the back edge, and a
     // value still pending from the prologue would put a vmcnt(0) -- draining
