@@ -183,14 +183,20 @@ def _fused_case(n, avg, seed, tail_frac=0.5):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,avg,mode", [(4096, 900, "range"), (1000, 3000, "grouped"), (70000, 200, "range"),
-                                        (150000, 200, "grouped"), (600000, 40, "range"), (600000, 40, "grouped")])
+                                        (150000, 200, "grouped"), (600000, 40, "range"), (600000, 40, "grouped"),
+                                        (1000, 3000, "declared"), (25000, 300, "declared"), (40000, 300, "declared"),
+                                        (150000, 200, "declared")])
 def test_fused_decrypt_and_frame(built, n, avg, mode):
     """zrc4_crypt_*_frame: decrypt the fresh tail and frame the WHOLE block in
     one launch: the direct kernels' epilogue at <= 1 group per CU, the
     persistent kernel's tail above (70 000 / 150 000 sessions: 274 / 587
     groups, one or two chunks per workgroup; 600 000: 2 344 groups, five
     chunks per workgroup, the tail's four-walk lockstep plus a remainder).
-    Plaintext and framing against the oracle."""
+    declared: zrc4_crypt_grouped_declared with framing, the engine's call --
+    6 buckets on the window kernel, ~100 and ~159 on crypt_decl_kernel
+    (half- and whole-group), ~587 behind the declared check on the
+    persistent kernel.  Plaintext and framing
+    against the oracle."""
     import torch
     from zsummerx_amd import Context
     from zsummerx_amd._capi import IDLE_SLOT
@@ -228,14 +234,21 @@ def test_fused_decrypt_and_frame(built, n, avg, mode):
             pk = torch.zeros(m * maxp, dtype=torch.int32, device="cuda")
             frame.update(off=T(np.array(fo, np.uint64).view(np.int64)), len=T(np.array(fl, np.uint32).view(np.int32)),
                          npk=npk, used=used, status=status, pkt_len=pk)
-            c.crypt_grouped_frame(d, T(np.array(eo, np.uint64).view(np.int64)),
-                                  T(np.array(el, np.uint32).view(np.int32)),
-                                  T(np.array(ids, np.uint32).view(np.int32)), frame)
+            args = (d, T(np.array(eo, np.uint64).view(np.int64)), T(np.array(el, np.uint32).view(np.int32)),
+                    T(np.array(ids, np.uint32).view(np.int32)))
+            if mode == "declared":
+                ida = np.full(-(-len(ids) // 256) * 256, IDLE_SLOT, np.uint32)    # (the last bucket is short)
+                ida[:len(ids)] = ids
+                ida = ida.reshape(-1, 256)
+                groups = np.where((ida != IDLE_SLOT).any(axis=1), ida.min(axis=1) // 256, IDLE_SLOT).astype(np.uint32)
+                c.crypt_grouped_declared(*args, groups, frame=frame)
+            else:
+                c.crypt_grouped_frame(*args, frame)
         c.sync()
         assert np.array_equal(d.cpu().numpy(), buf)
         got = [npk.cpu().numpy().view(np.uint32), used.cpu().numpy().view(np.uint32),
                status.cpu().numpy().view(np.uint32), pk.cpu().numpy().view(np.uint32).reshape(-1, maxp)]
-        if mode == "grouped":
+        if mode != "range":
             back = np.array(back)
             sel = back >= 0
             perm = np.empty(n, dtype=np.int64)
