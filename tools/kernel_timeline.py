@@ -95,9 +95,15 @@ def main():
     ap.add_argument("--active-waves", type=int, default=4,
                     help="only the first k waves of every 256-session group get payload (len 0 for the rest): "
                          "the chain rate at k waves per CU")
+    ap.add_argument("--define", action="append", default=[], help="extra -D for the timing build (NAME=V)")
     args = ap.parse_args()
     from zsummerx_amd import build
-    path = build.build_variant("timing", {"ZRC4_TIMING": "1"})
+    defs = {"ZRC4_TIMING": "1"}
+    for d in args.define:
+        k, _, v = d.partition("=")
+        defs[k] = v or "1"
+    name = "timing" + "".join(f"_{k}{v}" for k, v in sorted(defs.items()) if k != "ZRC4_TIMING")
+    path = build.build_variant(name, defs)
     if args.build_only:
         print("built", path)
         return

@@ -18,6 +18,7 @@
 #include "win_var.hpp"
 #include "win_repair.hpp"
 #include "win_var2.hpp"
+#include "win_var3.hpp"
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 constexpr int MAXN = (int)zrc4::kWinRing;   // keystream ring per stream (bytes)
@@ -426,6 +427,132 @@ win6_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint
     zrc4::WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     zrc4::win_windows(w, live ? (uint32_t)N : 0u, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
+                      (uint32_t)(uintptr_t)R);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((w.xa - 1) & 255) | ((w.y & 255) << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = (w.v >> 8) - 1;
+        }
+    }
+}
+
+// v17 (mode 17): variant S (tools/ubench/win_var3.hpp): J, d and x + 1 masked by SDWA byte writes
+// on a linear S-box layout: the tuning harness for the library kernel (the
+// loop uses only the first 256 bytes of each stream's 512-byte S area).
+__global__ void __launch_bounds__(64)
+win17_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+            uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int W = 16, SPW = 4;
+    __shared__ __attribute__((aligned(1024))) uint32_t Mk[SPW * 256];
+    __shared__ __attribute__((aligned(MAXN))) uint8_t Ring[SPW * MAXN];
+    __shared__ __attribute__((aligned(512))) uint8_t Sb[SPW * 512];
+    const uint32_t lane = threadIdx.x, l = lane % W, g = lane / W;
+    const int s = blockIdx.x * SPW + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 512;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        const uint8_t v = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        S[l * (256 / W) + k] = v;
+        S[256 + l * (256 / W) + k] = v;
+        M[l * (256 / W) + k] = 0;
+    }
+    const uint32_t sxy = live ? xy_in[s] : 0;
+    __syncthreads();
+    zrc4::WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    zrc4::win_windows_S(w, live ? (uint32_t)N : 0u, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
+                      (uint32_t)(uintptr_t)R);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((w.xa - 1) & 255) | ((w.y & 255) << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = (w.v >> 8) - 1;
+        }
+    }
+}
+
+// mode 18: variant Sae (tools/ubench/win_var3.hpp): J, d and x + 1 masked by SDWA byte writes
+// on a linear S-box layout: the tuning harness for the library kernel (the
+// loop uses only the first 256 bytes of each stream's 512-byte S area).
+__global__ void __launch_bounds__(64)
+win18_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+            uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int W = 16, SPW = 4;
+    __shared__ __attribute__((aligned(1024))) uint32_t Mk[SPW * 256];
+    __shared__ __attribute__((aligned(MAXN))) uint8_t Ring[SPW * MAXN];
+    __shared__ __attribute__((aligned(512))) uint8_t Sb[SPW * 512];
+    const uint32_t lane = threadIdx.x, l = lane % W, g = lane / W;
+    const int s = blockIdx.x * SPW + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 512;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        const uint8_t v = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        S[l * (256 / W) + k] = v;
+        S[256 + l * (256 / W) + k] = v;
+        M[l * (256 / W) + k] = 0;
+    }
+    const uint32_t sxy = live ? xy_in[s] : 0;
+    __syncthreads();
+    zrc4::WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    zrc4::win_windows_Sae(w, live ? (uint32_t)N : 0u, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
+                      (uint32_t)(uintptr_t)R);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (live) {
+        for (int k = 0; k < N / W; ++k) ks_out[(size_t)s * N + l * (N / W) + k] = R[l * (N / W) + k];
+        for (int k = 0; k < 256 / W; ++k) sbox_out[(size_t)s * 256 + l * (256 / W) + k] = S[l * (256 / W) + k];
+        if (l == 0) {
+            xy_out[s] = (uint16_t)(((w.xa - 1) & 255) | ((w.y & 255) << 8));
+            cyc[s] = t1 - t0;
+            wins[s] = (w.v >> 8) - 1;
+        }
+    }
+}
+
+// mode 19: variant Sbe (tools/ubench/win_var3.hpp): J, d and x + 1 masked by SDWA byte writes
+// on a linear S-box layout: the tuning harness for the library kernel (the
+// loop uses only the first 256 bytes of each stream's 512-byte S area).
+__global__ void __launch_bounds__(64)
+win19_kernel(const uint8_t *sbox_in, const uint16_t *xy_in, uint8_t *ks_out, uint8_t *sbox_out,
+            uint16_t *xy_out, uint64_t *cyc, uint32_t *wins, int nstreams, int N)
+{
+    constexpr int W = 16, SPW = 4;
+    __shared__ __attribute__((aligned(1024))) uint32_t Mk[SPW * 256];
+    __shared__ __attribute__((aligned(MAXN))) uint8_t Ring[SPW * MAXN];
+    __shared__ __attribute__((aligned(512))) uint8_t Sb[SPW * 512];
+    const uint32_t lane = threadIdx.x, l = lane % W, g = lane / W;
+    const int s = blockIdx.x * SPW + (int)g;
+    const bool live = s < nstreams;
+    uint8_t *S = Sb + g * 512;
+    uint32_t *M = Mk + g * 256;
+    uint8_t *R = Ring + g * MAXN;
+    for (int k = 0; k < 256 / W; ++k) {
+        const uint8_t v = live ? sbox_in[(size_t)s * 256 + l * (256 / W) + k] : 0;
+        S[l * (256 / W) + k] = v;
+        S[256 + l * (256 / W) + k] = v;
+        M[l * (256 / W) + k] = 0;
+    }
+    const uint32_t sxy = live ? xy_in[s] : 0;
+    __syncthreads();
+    zrc4::WinLane w{((sxy & 0xFFu) + 1u) & 0xFFu, sxy >> 8, (1u << 8) | (255u - l), l};
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    zrc4::win_windows_Sbe(w, live ? (uint32_t)N : 0u, l, (uint32_t)(uintptr_t)S, (uint32_t)(uintptr_t)M,
                       (uint32_t)(uintptr_t)R);
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     __syncthreads();
@@ -881,7 +1008,10 @@ static void run(int ns, int N, int reps)
     std::vector<float> ms;
     for (int r = 0; r < reps; ++r) {
         CHECK(hipEventRecord(e0));
-        if constexpr (V3 == 16) win16_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        if constexpr (V3 == 19) win19_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if constexpr (V3 == 18) win18_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if constexpr (V3 == 17) win17_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
+        else if constexpr (V3 == 16) win16_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if constexpr (V3 == 15) win15_kernel<<<(ns + 1) / 2, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if constexpr (V3 == 13) win13_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
         else if constexpr (V3 == 12) win12_kernel<<<(ns + 3) / 4, 64>>>(dsb, dxy, dks, dsbo, dxyo, dcyc, dwin, ns, N);
@@ -934,7 +1064,10 @@ int main(int argc, char **argv)
     const int wpb = argc > 4 ? atoi(argv[4]) : 1;
     if (N > MAXN || N % 16) { printf("bytes must be a multiple of 16 and <= %d\n", MAXN); return 1; }
     const int v3 = argc > 5 ? atoi(argv[5]) : 1;
-    if (v3 == 16) run<16, 1, 16>(ns, N, 20);
+    if (v3 == 19) run<16, 1, 19>(ns, N, 20);
+    else if (v3 == 18) run<16, 1, 18>(ns, N, 20);
+    else if (v3 == 17) run<16, 1, 17>(ns, N, 20);
+    else if (v3 == 16) run<16, 1, 16>(ns, N, 20);
     else if (v3 == 15) run<16, 1, 15>(ns, N, 20);
     else if (v3 == 13) run<16, 1, 13>(ns, N, 20);
     else if (v3 == 12) run<16, 1, 12>(ns, N, 20);

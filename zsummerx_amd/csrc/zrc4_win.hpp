@@ -83,6 +83,11 @@ struct WinLane {
 // accumulator chain read stale values on MI355X -- bit-exact only because the
 // wrong j always tripped the duplicate rule -- and the DPP scan needs no
 // window bytes at all.)
+// ZRC4_WIN_SDWA (A/B only): the masks of J, d and x + 1 folded into SDWA
+// byte writes (3 instructions less per window; tools/ubench win_var3.hpp).
+#ifndef ZRC4_WIN_SDWA
+#define ZRC4_WIN_SDWA 0
+#endif
 #define ZW_ADDR(XA)                                                                               \
     "v_add_u32_sdwa v106, " XA ", %[l] dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "  \
     "src1_sel:DWORD\n\t"
@@ -114,10 +119,17 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_cndmask_b32_e64 v124, v121, v122, s[42:43]\n\t"
         "v_add_u32_dpp v112, v112, v112 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_max_u32_dpp v120, v120, v120 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+#if ZRC4_WIN_SDWA
+        "v_add_u32_sdwa v112, v112, v120 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"   // J = scan + y' (mod 256)
+        // 2. b / marker round trip, d rule and rem cap under it
+        "v_and_b32 %[y], 0xff, v120\n\t"                      // (one op between the SDWA byte write and its readers)
+        "v_add_u32 v114, %[sb], v112\n\t"
+#else
         "v_add_u32 v112, v112, v120\n\t"                       // + y' (byte 0 of v120; J is masked below)
         // 2. b / marker round trip, d rule and rem cap under it
         "v_add_u32_sdwa v114, %[sb], v112 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"
         "v_and_b32 v112, 0xff, v112\n\t"                       // J
+#endif
         "v_lshl_add_u32 v115, v112, 2, %[mb]\n\t"
         "ds_read_u8 v116, v114\n\t"                             // b_l = S0[J]
         "ds_max_u32 v115, %[v]\n\t"
@@ -126,9 +138,14 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "s_mov_b64 exec, s[46:47]\n\t"
         "ds_write_b8 v125, v124\n\t"                            // window n-1's ring store, behind the round trip
         "s_mov_b64 exec, s[40:41]\n\t"
+#if ZRC4_WIN_SDWA
+        "v_sub_u32_sdwa v118, v112, %[xa] dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t"   // d
+        "v_or_b32 v130, %[l1], v112\n\t"                        // y' candidate of this lane (between)
+#else
         "v_and_b32 %[y], 0xff, v120\n\t"
         "v_sub_u32 v118, v112, %[xa]\n\t"
         "v_and_b32 v118, 0xff, v118\n\t"                       // d
+#endif
         "v_med3_u32 v119, v118, %[l], 16\n\t"
         "v_cmp_ne_u32 vcc, v118, %[l]\n\t"
         "v_cndmask_b32 v119, 16, v119, vcc\n\t"
@@ -137,7 +154,9 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_lshlrev_b32 v119, v119, 1\n\t"
         "v_or_b32 v118, v118, v119\n\t"                        // + bit min(rem, 16): cut <= rem
         "v_or_b32 v119, v118, %[bitl]\n\t"                     // the same if this lane's J repeats
+#if !ZRC4_WIN_SDWA
         "v_or_b32 v130, %[l1], v112\n\t"                        // y' candidate of this lane
+#endif
         "v_bfi_b32 v125, %[rmask], %[rp], %[rb]\n\t"            // ring slot of this lane
         "s_waitcnt lgkmcnt(1)\n\t"
         // 3. duplicate-J rule, OR over the stream's 16 lanes, cut
@@ -169,8 +188,12 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "ds_read_b32 v123, v129\n\t"                            // lowest lane whose J == t
         "s_and_b64 s[46:47], vcc, s[40:41]\n\t"                 // commit mask (ring store next iteration)
         "v_cndmask_b32 v120, %[y], v130, vcc\n\t"
+#if ZRC4_WIN_SDWA
+        "v_add_u32_sdwa %[xa], %[xa], v118 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD\n\t"
+#else
         "v_add_u32 %[xa], %[xa], v118\n\t"
         "v_and_b32 %[xa], 0xff, %[xa]\n\t"
+#endif
         "v_sub_u32 %[rem], %[rem], v118\n\t"
         "v_add_u32 %[rp], %[rp], v118\n\t"
         "v_cmp_ne_u32 vcc, 0, %[rem]\n\t"
