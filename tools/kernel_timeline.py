@@ -76,6 +76,11 @@ def placement(rec: np.ndarray, hwid: np.ndarray, act: np.ndarray, L: int) -> dic
             out["slow"].append({"wave": int(i), "cyc": round(float(cyc[i]), 2), "xcc": int(xcc[i]), "se": int(se[i]),
                                 "sh": int(sh[i]), "cu": int(cu[i]), "simd": int(simd[i])})
     out["slow"] = out["slow"][:24]
+    out["by_xcc"] = {int(x): {"waves": int(((xcc == x) & act).sum()),
+                              "med": round(float(np.median(cyc[(xcc == x) & act])), 2),
+                              "p90": round(float(np.percentile(cyc[(xcc == x) & act], 90)), 2),
+                              "max": round(float(cyc[(xcc == x) & act].max()), 2)}
+                     for x in np.unique(xcc[act])}
     out["all"] = [[int(xcc[i]), int(se[i]), int(sh[i]), int(cu[i]), int(simd[i]), round(float(cyc[i]), 1)]
                   for i in np.flatnonzero(act)][:256]
     return out
