@@ -347,6 +347,22 @@ __device__ __forceinline__ uint4 xor16(uint8_t *S, Rc4Lane &st, uint4 v)
     "v_add_u32_sdwa %[" #XN "], 1, %[" #XC "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "        \
     "src0_sel:DWORD src1_sel:BYTE_1\n\t"
 #endif
+// ZRC4_AB_LDS (timing-only ablations, outputs wrong): 1 drops the S[x] = b
+// write, 2 drops the keystream read S[t] -- how much the LDS pipe bounds the
+// step at 8 waves per CU.
+#ifndef ZRC4_AB_LDS
+#define ZRC4_AB_LDS 0
+#endif
+#if ZRC4_AB_LDS == 1
+#define ZRC4_CORE_XW(XC)
+#define ZRC4_CORE_KR(K) "s_waitcnt lgkmcnt(1)\n\t"
+#elif ZRC4_AB_LDS == 2
+#define ZRC4_CORE_XW(XC) "ds_write_b8 %[" #XC "], %[b]\n\t"
+#define ZRC4_CORE_KR(K) "s_waitcnt lgkmcnt(1)\n\t"
+#else
+#define ZRC4_CORE_XW(XC) "ds_write_b8 %[" #XC "], %[b]\n\t"
+#define ZRC4_CORE_KR(K) "ds_read_u8 %[" #K "], %[ta]\n\t" "s_waitcnt lgkmcnt(2)\n\t"
+#endif
 #define ZRC4_CORE(XC, XN, A, P, K)                                                               \
     "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
     "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
@@ -355,11 +371,10 @@ __device__ __forceinline__ uint4 xor16(uint8_t *S, Rc4Lane &st, uint4 v)
     ZRC4_XINC(XC, XN)                                                                            \
     "ds_read_u8 %[" #P "], %[" #XN "]\n\t"                                                       \
     "s_waitcnt lgkmcnt(2)\n\t"                                                                   \
-    "ds_write_b8 %[" #XC "], %[b]\n\t"                                                           \
+    ZRC4_CORE_XW(XC)                                                                             \
     "v_add_u32_sdwa %[ta], %[" #A "], %[b] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "           \
     "src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"                                                        \
-    "ds_read_u8 %[" #K "], %[ta]\n\t"                                                            \
-    "s_waitcnt lgkmcnt(2)\n\t"
+    ZRC4_CORE_KR(K)
 
 #define ZRC4_E ZRC4_CORE(x0, x1, a0, a1, k0)   // even step: keystream -> k0
 #define ZRC4_O ZRC4_CORE(x1, x0, a1, a0, k1)   // odd step:  keystream -> k1
