@@ -64,6 +64,30 @@ __device__ __forceinline__ uint32_t col_of(uint32_t j) {
 // step s even -> k0 (lane s % 4), XORed at step s + 1
 #define ZW ZE ZX(BYTE_3, k1) ZO ZX(BYTE_0, k0) ZE ZX(BYTE_1, k1) ZO ZX(BYTE_2, k0)
 
+// ------------------------------------- classic step with a byte exchange
+// b = S[y], S[y] = a in ONE LDS op: ds_mskor_rtn_b32 on the dword holding
+// the byte (clear mask m = 0xFF << 8*(col & 3), set a << 8*(col & 3)), the
+// old byte extracted with v_bfe.  yd = y's dword address (byte 1 updated
+// with y, byte 0 = col & ~3), sh = 8*(col & 3).
+#define MC(XC, XN, A, P, K)                                                                      \
+    "v_add_u32_sdwa %[ya], %[ya], %[" #A "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "          \
+    "src0_sel:BYTE_1 src1_sel:BYTE_0\n\t"                                                        \
+    "v_lshlrev_b32 %[tmp], %[sh], %[" #A "]\n\t"                                                \
+    "v_and_b32 %[yd], %[ya], %[nm3]\n\t"                                                        \
+    "ds_mskor_rtn_b32 %[b], %[yd], %[m], %[tmp]\n\t"                                            \
+    "v_add_u16_e32 %[" #XN "], %[c100], %[" #XC "]\n\t"                                          \
+    "ds_read_u8 %[" #P "], %[" #XN "]\n\t"                                                       \
+    "s_waitcnt lgkmcnt(1)\n\t"                                                                   \
+    "v_bfe_u32 %[b], %[b], %[sh], 8\n\t"                                                         \
+    "ds_write_b8 %[" #XC "], %[b]\n\t"                                                           \
+    "v_add_u32_sdwa %[ta], %[" #A "], %[b] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "           \
+    "src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"                                                        \
+    "ds_read_u8 %[" #K "], %[ta]\n\t"                                                            \
+    "s_waitcnt lgkmcnt(2)\n\t"
+#define ME MC(x0, x1, a0, a1, k0)
+#define MO MC(x1, x0, a1, a0, k1)
+#define MW ME ZX(BYTE_3, k1) MO ZX(BYTE_0, k0) ME ZX(BYTE_1, k1) MO ZX(BYTE_2, k0)
+
 // ------------------------------------------------------- pipelined step
 #define PS(XP, XC, XN, XF, AP, AC, AN, AF, BPP, BP, BC, SP, SC, KW, KX, LX)                       \
     "v_add_u32_sdwa %[ya], %[ya], %[" #AC "] dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "         \
@@ -134,6 +158,42 @@ __global__ void __launch_bounds__(256) classic_kernel(uint8_t *sout, Out *out, i
                      : [ya] "+v"(ya), [ta] "+v"(ta), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0),
                        [a1] "=&v"(a1), [b] "=&v"(b), [k0] "+v"(k0), [k1] "+v"(k1), [d] "+v"(d)
                      : [c100] "s"(c100) : "memory");
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+        out[g].cyc = t1 - t0;
+        out[g].d = d;
+        out[g].xy = ((x0 >> 8) & 255u) | (((ya >> 8) & 255u) << 8);   // the last step's x (its XC)
+    }
+    __syncthreads();
+    for (int k = 0; k < 256; ++k) sout[((size_t)blockIdx.x * 256 + threadIdx.x) * 256 + k] = S[(k << 8) | col];
+}
+
+// classic with the byte exchange (ds_mskor_rtn_b32): steps = 12 * blocks + 1
+__global__ void __launch_bounds__(256) mskor_kernel(uint8_t *sout, Out *out, int blocks, int active_waves)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t S[65536];
+    const uint32_t col = col_of(threadIdx.x);
+    init_s(S, col);
+    __syncthreads();
+    const bool act = (int)(threadIdx.x >> 6) < active_waves;
+    if (act) {
+        const uint32_t c100 = 0x100;
+        uint32_t ya = (7u << 8) | col, ta = col, x0 = col, x1 = col, a0 = S[x0], d = 0;   // x = 0: a0 = S[0]
+        uint32_t a1, b, k0 = 0, k1 = 0, tmp, yd;
+        const uint32_t sh = 8u * (col & 3u), m = 0xFFu << sh, nm3 = ~3u;
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        for (int i = 0; i < blocks; ++i) {
+            asm volatile(MW MW MW
+                         : [ya] "+v"(ya), [ta] "+v"(ta), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0),
+                           [a1] "=&v"(a1), [b] "=&v"(b), [k0] "+v"(k0), [k1] "+v"(k1), [d] "+v"(d),
+                           [tmp] "=&v"(tmp), [yd] "=&v"(yd)
+                         : [c100] "s"(c100), [sh] "v"(sh), [m] "v"(m), [nm3] "v"(nm3) : "memory");
+        }
+        asm volatile(ME ZX(BYTE_3, k1) "s_waitcnt lgkmcnt(0)\n\t" ZX(BYTE_0, k0)
+                     : [ya] "+v"(ya), [ta] "+v"(ta), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0),
+                       [a1] "=&v"(a1), [b] "=&v"(b), [k0] "+v"(k0), [k1] "+v"(k1), [d] "+v"(d),
+                       [tmp] "=&v"(tmp), [yd] "=&v"(yd)
+                     : [c100] "s"(c100), [sh] "v"(sh), [m] "v"(m), [nm3] "v"(nm3) : "memory");
         const uint64_t t1 = __builtin_amdgcn_s_memtime();
         const uint32_t g = blockIdx.x * 256 + threadIdx.x;
         out[g].cyc = t1 - t0;
@@ -231,24 +291,29 @@ int main(int argc, char **argv)
         CHECK(hipMalloc(&ds, (size_t)n * 256)); CHECK(hipMalloc(&dout, (size_t)n * sizeof(Out)));
         std::vector<uint8_t> s0((size_t)n * 256), s1((size_t)n * 256);
         std::vector<Out> o0(n), o1(n);
-        double med[2];
-        for (int v = 0; v < 2; ++v) {
+        std::vector<uint8_t> s2((size_t)n * 256);
+        std::vector<Out> o2(n);
+        double med[3];
+        for (int v = 0; v < 3; ++v) {
             CHECK(hipMemset(dout, 0, (size_t)n * sizeof(Out)));
             for (int r = 0; r < 3; ++r) {
                 if (v == 0) hipLaunchKernelGGL(classic_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
-                else hipLaunchKernelGGL(pipe_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
+                else if (v == 1) hipLaunchKernelGGL(pipe_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
+                else hipLaunchKernelGGL(mskor_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
                 CHECK(hipDeviceSynchronize());
             }
-            CHECK(hipMemcpy(v ? s1.data() : s0.data(), ds, (size_t)n * 256, hipMemcpyDeviceToHost));
-            CHECK(hipMemcpy(v ? o1.data() : o0.data(), dout, (size_t)n * sizeof(Out), hipMemcpyDeviceToHost));
+            std::vector<uint8_t> &sv = v == 0 ? s0 : v == 1 ? s1 : s2;
+            std::vector<Out> &ov = v == 0 ? o0 : v == 1 ? o1 : o2;
+            CHECK(hipMemcpy(sv.data(), ds, (size_t)n * 256, hipMemcpyDeviceToHost));
+            CHECK(hipMemcpy(ov.data(), dout, (size_t)n * sizeof(Out), hipMemcpyDeviceToHost));
             std::vector<double> cyc;
             for (int g = 0; g < n; ++g)
-                if ((int)((g % 256) >> 6) < c.waves) cyc.push_back((double)(v ? o1 : o0)[g].cyc / steps);
+                if ((int)((g % 256) >> 6) < c.waves) cyc.push_back((double)ov[g].cyc / steps);
             std::sort(cyc.begin(), cyc.end());
             med[v] = cyc[cyc.size() / 2];
         }
         // bit-exactness: classic vs CPU on a sample, pipelined vs classic everywhere (active lanes)
-        long bad_cpu = 0, bad_pipe = 0;
+        long bad_cpu = 0, bad_pipe = 0, bad_mskor = 0;
         std::vector<uint8_t> S(256);
         for (int g = 0; g < n; ++g) {
             if ((int)((g % 256) >> 6) >= c.waves) continue;
@@ -259,6 +324,8 @@ int main(int argc, char **argv)
             }
             if (memcmp(&s0[(size_t)g * 256], &s1[(size_t)g * 256], 256) || o0[g].d != o1[g].d || o0[g].xy != o1[g].xy)
                 ++bad_pipe;
+            if (memcmp(&s0[(size_t)g * 256], &s2[(size_t)g * 256], 256) || o0[g].d != o2[g].d || o0[g].xy != o2[g].xy)
+                ++bad_mskor;
         }
         if (getenv("PIPE_DEBUG")) {
             for (int g = 0; g < 3; ++g) {
@@ -271,7 +338,8 @@ int main(int argc, char **argv)
             }
         }
         printf(", \"%s\": {\"classic_cyc_per_byte\": %.1f, \"pipelined_cyc_per_byte\": %.1f, \"classic_vs_cpu_bad\": %ld, "
-               "\"pipelined_vs_classic_bad\": %ld}", c.name, med[0], med[1], bad_cpu, bad_pipe);
+               "\"pipelined_vs_classic_bad\": %ld, \"mskor_cyc_per_byte\": %.1f, \"mskor_vs_classic_bad\": %ld}",
+               c.name, med[0], med[1], bad_cpu, bad_pipe, med[2], bad_mskor);
         CHECK(hipFree(ds)); CHECK(hipFree(dout));
     }
     printf("}\n");
