@@ -168,6 +168,45 @@ __global__ void __launch_bounds__(256) classic_kernel(uint8_t *sout, Out *out, i
     for (int k = 0; k < 256; ++k) sout[((size_t)blockIdx.x * 256 + threadIdx.x) * 256 + k] = S[(k << 8) | col];
 }
 
+// classic with 32-lane waves: 512 threads, lanes 32-63 of every wave idle, so
+// a CU's 256 streams run on 8 waves (2 per SIMD) instead of 4: is one wave's
+// LDS instruction rate per instruction or per lane?
+__global__ void __launch_bounds__(512) half_kernel(uint8_t *sout, Out *out, int blocks, int active_waves)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t S[65536];
+    const uint32_t hj = (threadIdx.x >> 6) * 32u + (threadIdx.x & 31u);   // stream of this lane
+    const bool lane_on = (threadIdx.x & 63u) < 32u;
+    const uint32_t col = col_of(hj);
+    if (lane_on)
+        for (int k = 0; k < 256; ++k) S[(k << 8) | col] = (uint8_t)((k * 73 + hj) & 255);
+    __syncthreads();
+    const bool act = lane_on && (int)(threadIdx.x >> 6) < 2 * active_waves;
+    if (act) {
+        const uint32_t c100 = 0x100;
+        uint32_t ya = (7u << 8) | col, ta = col, x0 = col, x1 = col, a0 = S[x0], d = 0;   // x = 0: a0 = S[0]
+        uint32_t a1, b, k0 = 0, k1 = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        for (int i = 0; i < blocks; ++i) {
+            asm volatile(ZW ZW ZW
+                         : [ya] "+v"(ya), [ta] "+v"(ta), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0),
+                           [a1] "=&v"(a1), [b] "=&v"(b), [k0] "+v"(k0), [k1] "+v"(k1), [d] "+v"(d)
+                         : [c100] "s"(c100) : "memory");
+        }
+        asm volatile(ZE ZX(BYTE_3, k1) "s_waitcnt lgkmcnt(0)\n\t" ZX(BYTE_0, k0)
+                     : [ya] "+v"(ya), [ta] "+v"(ta), [x0] "+v"(x0), [x1] "+v"(x1), [a0] "+v"(a0),
+                       [a1] "=&v"(a1), [b] "=&v"(b), [k0] "+v"(k0), [k1] "+v"(k1), [d] "+v"(d)
+                     : [c100] "s"(c100) : "memory");
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        const uint32_t g = blockIdx.x * 256 + hj;
+        out[g].cyc = t1 - t0;
+        out[g].d = d;
+        out[g].xy = ((x0 >> 8) & 255u) | (((ya >> 8) & 255u) << 8);   // the last step's x (its XC)
+    }
+    __syncthreads();
+    if (lane_on)
+        for (int k = 0; k < 256; ++k) sout[((size_t)blockIdx.x * 256 + hj) * 256 + k] = S[(k << 8) | col];
+}
+
 // classic with the byte exchange (ds_mskor_rtn_b32): steps = 12 * blocks + 1
 __global__ void __launch_bounds__(256) mskor_kernel(uint8_t *sout, Out *out, int blocks, int active_waves)
 {
@@ -291,19 +330,20 @@ int main(int argc, char **argv)
         CHECK(hipMalloc(&ds, (size_t)n * 256)); CHECK(hipMalloc(&dout, (size_t)n * sizeof(Out)));
         std::vector<uint8_t> s0((size_t)n * 256), s1((size_t)n * 256);
         std::vector<Out> o0(n), o1(n);
-        std::vector<uint8_t> s2((size_t)n * 256);
-        std::vector<Out> o2(n);
-        double med[3];
-        for (int v = 0; v < 3; ++v) {
+        std::vector<uint8_t> s2((size_t)n * 256), s3((size_t)n * 256);
+        std::vector<Out> o2(n), o3(n);
+        double med[4];
+        for (int v = 0; v < 4; ++v) {
             CHECK(hipMemset(dout, 0, (size_t)n * sizeof(Out)));
             for (int r = 0; r < 3; ++r) {
                 if (v == 0) hipLaunchKernelGGL(classic_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
                 else if (v == 1) hipLaunchKernelGGL(pipe_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
-                else hipLaunchKernelGGL(mskor_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
+                else if (v == 2) hipLaunchKernelGGL(mskor_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
+                else hipLaunchKernelGGL(half_kernel, dim3(grid), dim3(512), 0, 0, ds, dout, blocks, c.waves);
                 CHECK(hipDeviceSynchronize());
             }
-            std::vector<uint8_t> &sv = v == 0 ? s0 : v == 1 ? s1 : s2;
-            std::vector<Out> &ov = v == 0 ? o0 : v == 1 ? o1 : o2;
+            std::vector<uint8_t> &sv = v == 0 ? s0 : v == 1 ? s1 : v == 2 ? s2 : s3;
+            std::vector<Out> &ov = v == 0 ? o0 : v == 1 ? o1 : v == 2 ? o2 : o3;
             CHECK(hipMemcpy(sv.data(), ds, (size_t)n * 256, hipMemcpyDeviceToHost));
             CHECK(hipMemcpy(ov.data(), dout, (size_t)n * sizeof(Out), hipMemcpyDeviceToHost));
             std::vector<double> cyc;
@@ -313,7 +353,7 @@ int main(int argc, char **argv)
             med[v] = cyc[cyc.size() / 2];
         }
         // bit-exactness: classic vs CPU on a sample, pipelined vs classic everywhere (active lanes)
-        long bad_cpu = 0, bad_pipe = 0, bad_mskor = 0;
+        long bad_cpu = 0, bad_pipe = 0, bad_mskor = 0, bad_half = 0;
         std::vector<uint8_t> S(256);
         for (int g = 0; g < n; ++g) {
             if ((int)((g % 256) >> 6) >= c.waves) continue;
@@ -326,6 +366,8 @@ int main(int argc, char **argv)
                 ++bad_pipe;
             if (memcmp(&s0[(size_t)g * 256], &s2[(size_t)g * 256], 256) || o0[g].d != o2[g].d || o0[g].xy != o2[g].xy)
                 ++bad_mskor;
+            if (memcmp(&s0[(size_t)g * 256], &s3[(size_t)g * 256], 256) || o0[g].d != o3[g].d || o0[g].xy != o3[g].xy)
+                ++bad_half;
         }
         if (getenv("PIPE_DEBUG")) {
             for (int g = 0; g < 3; ++g) {
@@ -338,8 +380,9 @@ int main(int argc, char **argv)
             }
         }
         printf(", \"%s\": {\"classic_cyc_per_byte\": %.1f, \"pipelined_cyc_per_byte\": %.1f, \"classic_vs_cpu_bad\": %ld, "
-               "\"pipelined_vs_classic_bad\": %ld, \"mskor_cyc_per_byte\": %.1f, \"mskor_vs_classic_bad\": %ld}",
-               c.name, med[0], med[1], bad_cpu, bad_pipe, med[2], bad_mskor);
+               "\"pipelined_vs_classic_bad\": %ld, \"mskor_cyc_per_byte\": %.1f, \"mskor_vs_classic_bad\": %ld, "
+               "\"half_lanes_2x_waves_cyc_per_byte\": %.1f, \"half_vs_classic_bad\": %ld}",
+               c.name, med[0], med[1], bad_cpu, bad_pipe, med[2], bad_mskor, med[3], bad_half);
         CHECK(hipFree(ds)); CHECK(hipFree(dout));
     }
     printf("}\n");
