@@ -2410,7 +2410,11 @@ crypt_stream_kernel(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
         preload_line0(P, ls, sk);
         // the claims' answers after these loads: compared earlier, the wait
         // for them would drain the loads issued behind them
+#if ZRC4_GR_PRECLAIM
         asm volatile("" : "+v"(old0) :: "memory");
+#else
+        asm volatile("" ::: "memory");
+#endif
 #else
         cur.len = bv.valid ? len[bv.ent] : 0u;
         cur.off = bv.valid ? off[bv.ent] : 0u;
