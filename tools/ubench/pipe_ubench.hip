@@ -127,6 +127,117 @@ __device__ __forceinline__ uint32_t col_of(uint32_t j) {
 #define P12 PS(X3, X0, X1, X2, A3, A0, A1, A2, B1, B2, B0, SG1, SG0, K0, K1, BYTE_2)
 #define P12STEPS P1 P2 P3 P4 P5 P6 P7 P8 P9 P10 P11 P12
 
+// ----------------------------------------------- consecutive-index layout
+// (r06): four consecutive S indices of one stream in one
+// dword, so one ds_read_b32 serves the four a = S[x] reads of a 4-byte block
+// and one ds_write_b32 retires its four S[x] = b writes.  Layout per 256-lane
+// group (64 KiB): byte (k >> 2) << 10 | lane << 2 | (k & 3), i.e. row m = k/4
+// holds one dword per lane: every ds_read_u8 / ds_read_b32 / ds_write_b32 of a
+// wave is bank-conflict free for any indices (bank = lane mod 32).
+// Registers: W = the current block's dword, kept as the TRUTH for S[4m..4m+3]
+// (LDS holds it stale until the block's dword write); XB = the block's dword
+// address (m << 10 | lane << 2); y8 = y as a clean byte.  Addresses are no
+// longer "index in byte 1" (the SDWA trick of the column layout): addr(v) =
+// (v * 0x101 & 0xFC03) | L, two VALU ops per computed index (y and t).
+// Exact step j (x = 4m + j), a = W.byte_j:
+//   y += a;  R = rotr(W, 8 (y & 3)) (R.b0 = W[y & 3]);  AY = addr(y)
+//   ds_read_u8 BR = S[AY];  ds_write_b8 S[AY] = a   (always: an in-block
+//   byte is overwritten by the dword write, an out-of-block one is final)
+//   c_y = (AY - XB) < 4 (y in this block)
+//   b = c_y ? R.b0 : BR;  t = a + b
+//   W' = W with byte (y & 3) = a (rotate, replace byte 0, rotate back);
+//   W = c_y ? W' : W;  W.byte_j = b      (S[x] = b then S[y] = a: the two
+//   bytes differ unless y == x, and then a == b)
+//   AT = addr(t);  ds_read_u8 KR = S[AT];  KW = W[t & 3];  c_t = (AT - XB) < 4
+//   k = c_t ? KW : KR   (finished in the next step, after its BR wait)
+// Block end: ds_write_b32 S[XB] = W; XB += 0x400 (16-bit wrap = index wrap);
+// ds_read_b32 W = S[XB] (waited for before the next block's first y add).
+// The skeleton (timing bound, outputs wrong) is the same LDS program and the
+// same address work without any patch: b = BR, k = KR, no in-block insert.
+#define QP_SEL(J) "%[sel" #J "]"
+#define QE_STEP(J, WD, JP, KRC, KWC, TCC, KRP, KWP, TCP)                                          \
+    "v_add_u32_sdwa %[y8], %[y8], %[w] dst_sel:BYTE_0 dst_unused:UNUSED_PAD "                    \
+    "src0_sel:BYTE_0 src1_sel:BYTE_" #J "\n\t"                                                   \
+    "v_alignbyte_b32 %[r], %[w], %[w], %[y8]\n\t" /* reads y8[1:0] only */                       \
+    QV_##J                                                                                       \
+    "v_lshl_or_b32 %[ay], %[y8], 8, %[y8]\n\t"                                                   \
+    "v_and_or_b32 %[ay], %[ay], %[msk], %[lb]\n\t"                                               \
+    "ds_read_u8 %[br], %[ay]\n\t"                                                                \
+    WD                                                                                           \
+    "v_sub_u32_e32 %[e], %[ay], %[xb]\n\t"                                                       \
+    "v_perm_b32 %[r2], %[w], %[r], " QP_SEL(J) "\n\t"                                            \
+    "v_sub_u32_e32 %[ny], 0, %[y8]\n\t"                                                          \
+    "v_cmp_gt_u32_e32 vcc, 4, %[e]\n\t"                                                          \
+    "v_alignbyte_b32 %[wi], %[r2], %[r2], %[ny]\n\t"                                             \
+    "s_waitcnt lgkmcnt(1)\n\t"                                                                   \
+    "v_cndmask_b32_e64 %[k], %[" #KRP "], %[" #KWP "], %[" #TCP "]\n\t"                          \
+    "v_cndmask_b32_e32 %[b], %[br], %[r], vcc\n\t"                                               \
+    "v_xor_b32_sdwa %[d], %[d], %[k] dst_sel:BYTE_" #JP " dst_unused:UNUSED_PRESERVE "           \
+    "src0_sel:BYTE_" #JP " src1_sel:BYTE_0\n\t"                                                  \
+    "v_add_u32_sdwa %[t8], %[w], %[b] dst_sel:BYTE_0 dst_unused:UNUSED_PAD "                     \
+    "src0_sel:BYTE_" #J " src1_sel:BYTE_0\n\t"                                                   \
+    "v_cndmask_b32_e32 %[w], %[w], %[wi], vcc\n\t"                                               \
+    "v_mov_b32_sdwa %[w], %[b] dst_sel:BYTE_" #J " dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0\n\t" \
+    "v_lshl_or_b32 %[at], %[t8], 8, %[t8]\n\t"                                                   \
+    "v_and_or_b32 %[at], %[at], %[msk], %[lb]\n\t"                                               \
+    "ds_read_u8 %[" #KRC "], %[at]\n\t"                                                          \
+    "v_sub_u32_e32 %[et], %[at], %[xb]\n\t"                                                      \
+    "v_alignbyte_b32 %[" #KWC "], %[w], %[w], %[t8]\n\t"                                         \
+    "v_cmp_gt_u32_e64 %[" #TCC "], 4, %[et]\n\t"
+// V = W >> 8 before the odd steps: their a sits in V's byte 0 / byte 2
+#define QV_0
+#define QV_1 "v_lshrrev_b32_e32 %[v], 8, %[w]\n\t"
+#define QV_2
+#define QV_3 "v_lshrrev_b32_e32 %[v], 8, %[w]\n\t"
+#define QWD_0 "ds_write_b8 %[ay], %[w]\n\t"
+#define QWD_1 "ds_write_b8 %[ay], %[v]\n\t"
+#define QWD_2 "ds_write_b8_d16_hi %[ay], %[w]\n\t"
+#define QWD_3 "ds_write_b8_d16_hi %[ay], %[v]\n\t"
+#define QE_BLOCK                                                                                 \
+    QE_STEP(0, QWD_0, 3, kr0, kw0, tc0, kr1, kw1, tc1)                                           \
+    QE_STEP(1, QWD_1, 0, kr1, kw1, tc1, kr0, kw0, tc0)                                           \
+    QE_STEP(2, QWD_2, 1, kr0, kw0, tc0, kr1, kw1, tc1)                                           \
+    QE_STEP(3, QWD_3, 2, kr1, kw1, tc1, kr0, kw0, tc0)                                           \
+    QBLOCK_END
+#define QBLOCK_END                                                                               \
+    "ds_write_b32 %[xb], %[w]\n\t"                                                               \
+    "v_add_u16_e32 %[xb], %[c400], %[xb]\n\t"                                                    \
+    "ds_read_b32 %[w], %[xb]\n\t"                                                                \
+    "s_waitcnt lgkmcnt(0)\n\t"
+// skeleton: same LDS program and address work, no patches (timing only)
+#define QK_STEP(J, WD, JP, KRC, KRP)                                                              \
+    "v_add_u32_sdwa %[y8], %[y8], %[w] dst_sel:BYTE_0 dst_unused:UNUSED_PAD "                    \
+    "src0_sel:BYTE_0 src1_sel:BYTE_" #J "\n\t"                                                   \
+    "v_lshrrev_b32_e32 %[v], 8, %[w]\n\t"                                                        \
+    "v_lshl_or_b32 %[ay], %[y8], 8, %[y8]\n\t"                                                   \
+    "v_and_or_b32 %[ay], %[ay], %[msk], %[lb]\n\t"                                               \
+    "ds_read_u8 %[br], %[ay]\n\t"                                                                \
+    WD                                                                                           \
+    "s_waitcnt lgkmcnt(1)\n\t"                                                                   \
+    "v_xor_b32_sdwa %[d], %[d], %[" #KRP "] dst_sel:BYTE_" #JP " dst_unused:UNUSED_PRESERVE "    \
+    "src0_sel:BYTE_" #JP " src1_sel:BYTE_0\n\t"                                                  \
+    "v_add_u32_sdwa %[t8], %[w], %[br] dst_sel:BYTE_0 dst_unused:UNUSED_PAD "                    \
+    "src0_sel:BYTE_" #J " src1_sel:BYTE_0\n\t"                                                   \
+    "v_mov_b32_sdwa %[w], %[br] dst_sel:BYTE_" #J " dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0\n\t" \
+    "v_lshl_or_b32 %[at], %[t8], 8, %[t8]\n\t"                                                   \
+    "v_and_or_b32 %[at], %[at], %[msk], %[lb]\n\t"                                               \
+    "ds_read_u8 %[" #KRC "], %[at]\n\t"
+#define QK_BLOCK                                                                                 \
+    QK_STEP(0, QWD_0, 3, kr0, kr1) QK_STEP(1, QWD_1, 0, kr1, kr0)                                \
+    QK_STEP(2, QWD_2, 1, kr0, kr1) QK_STEP(3, QWD_3, 2, kr1, kr0)                                \
+    QBLOCK_END
+// skeleton with the next block's dword read issued after step 1 (an exact
+// version would have to patch it for steps 1-3's writes into that block):
+// no round trip exposed at the block boundary -- the LDS program's best case
+#define QK2_BLOCK                                                                                \
+    QK_STEP(0, QWD_0, 3, kr0, kr1) QK_STEP(1, QWD_1, 0, kr1, kr0)                                \
+    "v_add_u16_e32 %[e], %[c400], %[xb]\n\t"                                                     \
+    "ds_read_b32 %[wi], %[e]\n\t"                                                                \
+    QK_STEP(2, QWD_2, 1, kr0, kr1) QK_STEP(3, QWD_3, 2, kr1, kr0)                                \
+    "ds_write_b32 %[xb], %[w]\n\t"                                                               \
+    "v_mov_b32_e32 %[xb], %[e]\n\t"                                                              \
+    "v_mov_b32_e32 %[w], %[wi]\n\t"
+
 struct Out { uint64_t cyc; uint32_t d, xy; };
 
 // The same state for every variant: S column = (k * 73 + tid) & 255, x = 0, y = 7.
@@ -295,6 +406,71 @@ __global__ void __launch_bounds__(256) pipe_kernel(uint8_t *sout, Out *out, int 
     for (int k = 0; k < 256; ++k) sout[((size_t)blockIdx.x * 256 + threadIdx.x) * 256 + k] = S[(k << 8) | col];
 }
 
+// consecutive-index layout: steps 0 .. 12 * blocks - 1 in 4-byte blocks, then
+// step 12 * blocks (j = 0 of the next block) and the final dword write.
+__device__ __forceinline__ uint32_t qaddr(uint32_t k, uint32_t j) { return ((k >> 2) << 10) | (j << 2) | (k & 3u); }
+
+#define QREGS                                                                                    \
+    [y8] "+v"(y8), [w] "+v"(w), [xb] "+v"(xb), [v] "+v"(v), [d] "+v"(d), [k] "+v"(k),          \
+    [kr0] "+v"(kr0), [kr1] "+v"(kr1), [kw0] "+v"(kw0), [kw1] "+v"(kw1), [tc0] "+s"(tc0),        \
+    [tc1] "+s"(tc1), [br] "=&v"(br), [b] "=&v"(b), [r] "=&v"(r), [r2] "=&v"(r2), [ny] "=&v"(ny), \
+    [wi] "=&v"(wi), [e] "=&v"(e), [t8] "=&v"(t8), [at] "=&v"(at), [et] "=&v"(et), [ay] "=&v"(ay)
+#define QINS                                                                                     \
+    [lb] "v"(lb), [msk] "s"(msk), [c400] "s"(c400), [sel0] "s"(sel0), [sel1] "s"(sel1),         \
+    [sel2] "s"(sel2), [sel3] "s"(sel3)
+
+template <int QMODE>   // 0 skeleton, 1 exact, 2 skeleton with the next block's read ahead
+__global__ void __launch_bounds__(256) quad_kernel(uint8_t *sout, Out *out, int blocks, int active_waves)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t S[65536];
+    const uint32_t jl = threadIdx.x;
+    for (int kk = 0; kk < 256; ++kk) S[qaddr(kk, jl)] = (uint8_t)((kk * 73 + jl) & 255);
+    __syncthreads();
+    const bool act = (int)(threadIdx.x >> 6) < active_waves;
+    if (act) {
+        const uint32_t lb = jl << 2, msk = 0xFC03u, c400 = 0x400u;
+        const uint32_t sel0 = 0x03020104u, sel1 = 0x03020105u, sel2 = 0x03020106u, sel3 = 0x03020107u;
+        uint32_t xb = lb, y8 = 7, d = 0, v = 0, k = 0, kr0 = 0, kr1 = 0, kw0 = 0, kw1 = 0;
+        uint32_t br, b, r, r2, ny, wi, e, t8, at, et, ay;
+        uint64_t tc0 = 0, tc1 = 0;
+        uint32_t w = *reinterpret_cast<const uint32_t *>(&S[xb]);      // x = 0: S[0..3]
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        for (int i = 0; i < blocks; ++i) {
+            if (QMODE == 1)
+                asm volatile(QE_BLOCK QE_BLOCK QE_BLOCK : QREGS : QINS : "memory", "vcc");
+            else if (QMODE == 2)
+                asm volatile(QK2_BLOCK QK2_BLOCK QK2_BLOCK : QREGS : QINS : "memory", "vcc");
+            else
+                asm volatile(QK_BLOCK QK_BLOCK QK_BLOCK : QREGS : QINS : "memory", "vcc");
+        }
+        if (QMODE == 1)
+            asm volatile(QE_STEP(0, QWD_0, 3, kr0, kw0, tc0, kr1, kw1, tc1)
+                         "s_waitcnt lgkmcnt(0)\n\t"
+                         "v_cndmask_b32_e64 %[k], %[kr0], %[kw0], %[tc0]\n\t"
+                         "s_nop 1\n\t"
+                         "v_xor_b32_sdwa %[d], %[d], %[k] dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE "
+                         "src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+                         "ds_write_b32 %[xb], %[w]\n\t"
+                         "s_waitcnt lgkmcnt(0)\n\t"
+                         : QREGS : QINS : "memory", "vcc");
+        else
+            asm volatile(QK_STEP(0, QWD_0, 3, kr0, kr1)
+                         "s_waitcnt lgkmcnt(0)\n\t"
+                         "v_xor_b32_sdwa %[d], %[d], %[kr0] dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE "
+                         "src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+                         "ds_write_b32 %[xb], %[w]\n\t"
+                         "s_waitcnt lgkmcnt(0)\n\t"
+                         : QREGS : QINS : "memory", "vcc");
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+        out[g].cyc = t1 - t0;
+        out[g].d = d;
+        out[g].xy = (((xb >> 10) & 63u) << 2) | ((y8 & 255u) << 8);
+    }
+    __syncthreads();
+    for (int kk = 0; kk < 256; ++kk) sout[((size_t)blockIdx.x * 256 + threadIdx.x) * 256 + kk] = S[qaddr(kk, jl)];
+}
+
 // CPU reference for one lane (tid t): same init, steps 12 * blocks + 1.
 static void cpu_ref(uint32_t t, int steps, uint8_t *S, uint32_t &d, uint32_t &xy)
 {
@@ -330,20 +506,26 @@ int main(int argc, char **argv)
         CHECK(hipMalloc(&ds, (size_t)n * 256)); CHECK(hipMalloc(&dout, (size_t)n * sizeof(Out)));
         std::vector<uint8_t> s0((size_t)n * 256), s1((size_t)n * 256);
         std::vector<Out> o0(n), o1(n);
-        std::vector<uint8_t> s2((size_t)n * 256), s3((size_t)n * 256);
-        std::vector<Out> o2(n), o3(n);
-        double med[4];
-        for (int v = 0; v < 4; ++v) {
+        std::vector<uint8_t> s2((size_t)n * 256), s3((size_t)n * 256), s4((size_t)n * 256), s5((size_t)n * 256), s6((size_t)n * 256);
+        std::vector<Out> o2(n), o3(n), o4(n), o5(n), o6(n);
+        double med[7];
+        // QUAD_ONLY: the classic step and the two consecutive-index kernels only
+        const bool quad_only = getenv("QUAD_ONLY") != nullptr;
+        for (int v = 0; v < 7; ++v) {
+            if (quad_only && v >= 1 && v <= 3) { med[v] = 0; continue; }
             CHECK(hipMemset(dout, 0, (size_t)n * sizeof(Out)));
             for (int r = 0; r < 3; ++r) {
                 if (v == 0) hipLaunchKernelGGL(classic_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
                 else if (v == 1) hipLaunchKernelGGL(pipe_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
                 else if (v == 2) hipLaunchKernelGGL(mskor_kernel, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
-                else hipLaunchKernelGGL(half_kernel, dim3(grid), dim3(512), 0, 0, ds, dout, blocks, c.waves);
+                else if (v == 3) hipLaunchKernelGGL(half_kernel, dim3(grid), dim3(512), 0, 0, ds, dout, blocks, c.waves);
+                else if (v == 4) hipLaunchKernelGGL(quad_kernel<1>, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
+                else if (v == 5) hipLaunchKernelGGL(quad_kernel<0>, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
+                else hipLaunchKernelGGL(quad_kernel<2>, dim3(grid), dim3(256), 0, 0, ds, dout, blocks, c.waves);
                 CHECK(hipDeviceSynchronize());
             }
-            std::vector<uint8_t> &sv = v == 0 ? s0 : v == 1 ? s1 : v == 2 ? s2 : s3;
-            std::vector<Out> &ov = v == 0 ? o0 : v == 1 ? o1 : v == 2 ? o2 : o3;
+            std::vector<uint8_t> &sv = v == 0 ? s0 : v == 1 ? s1 : v == 2 ? s2 : v == 3 ? s3 : v == 4 ? s4 : v == 5 ? s5 : s6;
+            std::vector<Out> &ov = v == 0 ? o0 : v == 1 ? o1 : v == 2 ? o2 : v == 3 ? o3 : v == 4 ? o4 : v == 5 ? o5 : o6;
             CHECK(hipMemcpy(sv.data(), ds, (size_t)n * 256, hipMemcpyDeviceToHost));
             CHECK(hipMemcpy(ov.data(), dout, (size_t)n * sizeof(Out), hipMemcpyDeviceToHost));
             std::vector<double> cyc;
@@ -353,7 +535,7 @@ int main(int argc, char **argv)
             med[v] = cyc[cyc.size() / 2];
         }
         // bit-exactness: classic vs CPU on a sample, pipelined vs classic everywhere (active lanes)
-        long bad_cpu = 0, bad_pipe = 0, bad_mskor = 0, bad_half = 0;
+        long bad_cpu = 0, bad_pipe = 0, bad_mskor = 0, bad_half = 0, bad_quad = 0, bad_quad_cpu = 0;
         std::vector<uint8_t> S(256);
         for (int g = 0; g < n; ++g) {
             if ((int)((g % 256) >> 6) >= c.waves) continue;
@@ -361,7 +543,11 @@ int main(int argc, char **argv)
                 uint32_t d, xy;
                 cpu_ref((uint32_t)(g % 256), steps, S.data(), d, xy);
                 if (memcmp(S.data(), &s0[(size_t)g * 256], 256) || d != o0[g].d || xy != o0[g].xy) ++bad_cpu;
+                if (memcmp(S.data(), &s4[(size_t)g * 256], 256) || d != o4[g].d || xy != o4[g].xy) ++bad_quad_cpu;
             }
+            if (memcmp(&s0[(size_t)g * 256], &s4[(size_t)g * 256], 256) || o0[g].d != o4[g].d || o0[g].xy != o4[g].xy)
+                ++bad_quad;
+            if (quad_only) continue;
             if (memcmp(&s0[(size_t)g * 256], &s1[(size_t)g * 256], 256) || o0[g].d != o1[g].d || o0[g].xy != o1[g].xy)
                 ++bad_pipe;
             if (memcmp(&s0[(size_t)g * 256], &s2[(size_t)g * 256], 256) || o0[g].d != o2[g].d || o0[g].xy != o2[g].xy)
@@ -373,16 +559,24 @@ int main(int argc, char **argv)
             for (int g = 0; g < 3; ++g) {
                 uint32_t d, xy;
                 cpu_ref((uint32_t)(g % 256), steps, S.data(), d, xy);
-                int fs0 = -1, fs1 = -1;
-                for (int k = 0; k < 256; ++k) { if (fs0 < 0 && s0[(size_t)g * 256 + k] != S[k]) fs0 = k; if (fs1 < 0 && s1[(size_t)g * 256 + k] != S[k]) fs1 = k; }
-                printf("\n  lane %d cpu d %08x xy %04x | classic d %08x xy %04x firstbadS %d | pipe d %08x xy %04x firstbadS %d", g, d, xy,
-                       o0[g].d, o0[g].xy, fs0, o1[g].d, o1[g].xy, fs1);
+                int fs0 = -1, fs1 = -1, fs4 = -1;
+                for (int k = 0; k < 256; ++k) {
+                    if (fs0 < 0 && s0[(size_t)g * 256 + k] != S[k]) fs0 = k;
+                    if (fs1 < 0 && s1[(size_t)g * 256 + k] != S[k]) fs1 = k;
+                    if (fs4 < 0 && s4[(size_t)g * 256 + k] != S[k]) fs4 = k;
+                }
+                printf("\n  lane %d cpu d %08x xy %04x | classic d %08x xy %04x firstbadS %d | pipe d %08x xy %04x firstbadS %d"
+                       " | quad d %08x xy %04x firstbadS %d", g, d, xy,
+                       o0[g].d, o0[g].xy, fs0, o1[g].d, o1[g].xy, fs1, o4[g].d, o4[g].xy, fs4);
             }
         }
         printf(", \"%s\": {\"classic_cyc_per_byte\": %.1f, \"pipelined_cyc_per_byte\": %.1f, \"classic_vs_cpu_bad\": %ld, "
                "\"pipelined_vs_classic_bad\": %ld, \"mskor_cyc_per_byte\": %.1f, \"mskor_vs_classic_bad\": %ld, "
-               "\"half_lanes_2x_waves_cyc_per_byte\": %.1f, \"half_vs_classic_bad\": %ld}",
-               c.name, med[0], med[1], bad_cpu, bad_pipe, med[2], bad_mskor, med[3], bad_half);
+               "\"half_lanes_2x_waves_cyc_per_byte\": %.1f, \"half_vs_classic_bad\": %ld, "
+               "\"quad_exact_cyc_per_byte\": %.1f, \"quad_exact_vs_classic_bad\": %ld, \"quad_exact_vs_cpu_bad\": %ld, "
+               "\"quad_skeleton_cyc_per_byte\": %.1f, \"quad_skeleton_read_ahead_cyc_per_byte\": %.1f}",
+               c.name, med[0], med[1], bad_cpu, bad_pipe, med[2], bad_mskor, med[3], bad_half,
+               med[4], bad_quad, bad_quad_cpu, med[5], med[6]);
         CHECK(hipFree(ds)); CHECK(hipFree(dout));
     }
     printf("}\n");
