@@ -130,19 +130,24 @@ class GpuRunner:
             # ids, as an engine's free list hands them out).  grouped: entries
             # bucketed by group -> zrc4_crypt_grouped (coalesced images);
             # scattered: the same ids unbucketed -> zrc4_crypt (per-lane gathers).
-            # (whole groups only: a short group placed mid-batch would make
-            # later buckets straddle two groups)
-            if S % 256:
+            # (grouped / declared: whole groups only -- a short group placed
+            # mid-batch would make later buckets straddle two groups; scattered
+            # ids are unbucketed, so a ragged last group is fine there)
+            if S % 256 and ids_mode != "scattered":
                 raise SystemExit(f"--ids {ids_mode} needs a multiple of 256 sessions per batch, not {S}")
             rng = np.random.default_rng(77)
             perm = np.empty(n, dtype=np.int64)
             bgroups = []
+            ng = -(-S // 256)
             for b in range(R):
-                order = rng.permutation(S // 256)
-                bgroups.append(np.ascontiguousarray((b * S // 256 + order).astype(np.uint32)))
-                for k, g in enumerate(order):
+                order = rng.permutation(ng)
+                bgroups.append(np.ascontiguousarray((b * ng + order).astype(np.uint32)))
+                pos = b * S
+                for g in order:
                     lo = b * S + g * 256
-                    perm[b * S + 256 * k: b * S + 256 * (k + 1)] = lo + rng.permutation(256)
+                    hi = min(lo + 256, (b + 1) * S)
+                    perm[pos:pos + hi - lo] = lo + rng.permutation(hi - lo)
+                    pos += hi - lo
             # entry e of batch b -> session perm[e]: keys/state/payload follow the session
             self.ids = T(perm.astype(np.int32))
             self.off = T((perm * L).astype(np.int64))
@@ -814,6 +819,9 @@ def parse(argv=None):
     p.add_argument("--companion-workload", choices=sorted(CONFIG_SHAPES) + ["none"], default="cfg5",
                    help="with the default weak cfg2 line: also measure this workload split over the same ranks "
                         "(strong scaling, BASELINE configs[4]) as 'configs4_strong'; none disables")
+    p.add_argument("--no-shard-projection", dest="shard_projection", action="store_false",
+                   help="N=1 only: skip timing the companion's 2/4/8-GPU shards on this GPU "
+                        "(configs4_strong.shard_projection)")
     p.add_argument("--companion-steps", type=int, default=100)
     p.add_argument("--companion-warmup", type=int, default=120)
     p.add_argument("--chunks", type=int, default=0,
@@ -894,6 +902,9 @@ def companion_strong(args, ws, rank, local, backend="nccl", make_runner=None):
     c.steps = max(args.steps, args.companion_steps)
     c.warmup = max(args.warmup, args.companion_warmup)
     res, runner = run_bench(c, ws, rank, local, backend, make_runner, own_pg=False)
+    proj = None
+    if ws == 1 and make_runner is None and getattr(args, "shard_projection", True) and res is not None:
+        proj = shard_projection(c, runner, res)
     if hasattr(runner, "close"):
         runner.close()
     if res is None:
@@ -905,6 +916,59 @@ def companion_strong(args, ws, rank, local, backend="nccl", make_runner=None):
     out["roofline"] = {k: res["roofline"][k] for k in ("achieved", "peak", "unit", "frac", "kernel",
                                                        "algorithmic_bytes_per_launch", "kernel_avg_us")}
     out["per_gpu"] = res["per_gpu"]
+    if proj is not None:
+        out["shard_projection"] = proj
+    return out
+
+
+def shard_projection(c, runner, res, gpus=(2, 4, 8)):
+    """SURVEY.md §8e on one GPU: the per-GPU shard of the strong configs[4]
+    split at N = 2, 4, 8 (524 288 / N sessions x 1 KiB), timed in the same
+    job as the 1-GPU line with the same method (warmup, then HIP events over
+    16-launch segments plus the sync-bracketed wall clock).  The shards are
+    contiguous slot ranges of the companion's own batch, launched in rotation
+    (shard k of N = slots [k S/N, (k+1) S/N)), so the rotation still covers the
+    whole >= 640 MiB footprint.  Speed-ups are against the 1-GPU value measured
+    just before: what N GPUs give if each runs its shard as this GPU does (no
+    collective on the data path; the driver's SCALE run measures the real
+    node)."""
+    if runner.R != 1 or runner._fn.__name__ != "zrc4_crypt_range":
+        return None
+    h, first, pay, offp, lenp, S, st = runner._args[0]
+    one_kern = res["roofline"]["kernel_avg_us"]
+    one_step = res["ms_per_step"] * 1e3
+    out = {"method": (f"{c.workload} shards of the 1-GPU batch on this GPU, rotated; {c.warmup} warmup "
+                      f"launches, then {c.steps} timed: HIP events over {c.event_every}-launch segments"),
+           "one_gpu_kernel_avg_us": one_kern, "one_gpu_us_per_step": round(one_step, 3), "shards": []}
+    saved = (runner._args, runner.R)
+    try:
+        for n in gpus:
+            if S % (256 * n):
+                continue
+            sn = S // n
+            runner._args = [(h, first + k * sn, pay, C.c_void_p(offp.value + 8 * k * sn),
+                             C.c_void_p(lenp.value + 4 * k * sn), sn, st) for k in range(n)]
+            runner.R = n
+            for i in range(c.warmup):
+                runner.step(i)
+            runner.sync()
+            marks = runner.make_events(c.steps, c.event_every)
+            t0 = time.perf_counter()
+            runner.launch_steps(c.warmup, c.steps, c.event_every, marks)
+            runner.sync()
+            wall = time.perf_counter() - t0
+            kern = statistics.mean(runner.segment_ms(c.steps, c.event_every, marks)) * 1e3
+            B = algorithmic_bytes(sn, runner.L)
+            out["shards"].append({
+                "gpus": n, "sessions_per_gpu": sn, "kernel_avg_us": round(kern, 3),
+                "us_per_step": round(wall / c.steps * 1e6, 3),
+                "achieved_gbs": round(B / (kern * 1e-6) / 1e9, 2),
+                "projected_speedup_kernel": round(one_kern / kern, 3),
+                "projected_speedup_step": round(one_step / (wall / c.steps * 1e6), 3),
+                "projected_job_gibs": round(n * sn * runner.L / (wall / c.steps) / GIB, 1)})
+        runner.check()
+    finally:
+        runner._args, runner.R = saved
     return out
 
 

@@ -124,13 +124,15 @@ int zrc4_crypt_range(zrc4_ctx *ctx, uint32_t first_slot, uint8_t *payload,
  *     claimant of a part runs.  Claims and refusals therefore apply per part:
  *     two buckets naming one group may each run some parts of it (each slot
  *     is still all or nothing: crypted with its state advanced, or untouched).
- *     A claim may be taken before the bucket's own check completes: on the
- *     kernels with at most one bucket per CU it is taken on the bucket's
- *     first busy id while the check runs, and on the persistent kernel
- *     (more buckets than CUs) a bucket that names one slot twice claims its
- *     group before its slot table refuses it.  So a bucket that breaks the
- *     one-group or once-per-slot rule may also block a valid bucket of a
- *     group it names.
+ *     Where the claim is taken: the window kernel (<= 32 buckets) claims
+ *     only after its bucket's table check has passed, so a bucket it
+ *     refuses claims nothing.  The half- and whole-group kernels (at most
+ *     one bucket per CU) claim while the check runs, on the bucket's first
+ *     busy id (zrc4_crypt_grouped_declared: on the declared group), and the
+ *     persistent kernel (more buckets than CUs) claims a bucket's group
+ *     before its slot table can refuse a slot named twice.  So on those
+ *     kernels a bucket that breaks the one-group or once-per-slot rule may
+ *     also block a valid bucket of a group it names.
  * An id >= capacity other than ZRC4_IDLE_SLOT is skipped and reported as
  * ZRC4_ERR_SLOT_RANGE (the rest of its bucket runs).  The claims carry a
  * per-call tag chosen on the host: a grouped call must not be captured into

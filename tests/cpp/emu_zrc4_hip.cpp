@@ -112,6 +112,7 @@ int zrc4_crypt_grouped_declared(zrc4_ctx *c, const uint32_t *ids, const uint32_t
     for (uint32_t b = 0; b < (n + 255) / 256; ++b)
         if (bg[b] >= groups && bg[b] != ZRC4_IDLE_SLOT) return ZRC4_ERR_INVALID_ARG;
     std::vector<uint32_t> kept(ids, ids + n);
+    std::vector<uint32_t> lost;           // groups a disagreeing bucket's ids name
     int rc = ZRC4_OK;
     for (uint32_t b = 0; b < n; b += 256) {
         const uint32_t e = b + 256 < n ? b + 256 : n;
@@ -120,6 +121,21 @@ int zrc4_crypt_grouped_declared(zrc4_ctx *c, const uint32_t *ids, const uint32_t
             if (len[i] && ids[i] != ZRC4_IDLE_SLOT && ids[i] < c->st.size() && ids[i] / 256 != bg[b / 256]) bad = true;
         if (bad) {
             rc = ZRC4_ERR_GROUP;
+            for (uint32_t i = b; i < e; ++i) {
+                if (len[i] && ids[i] != ZRC4_IDLE_SLOT && ids[i] < c->st.size()) lost.push_back(ids[i] / 256);
+                kept[i] = ZRC4_IDLE_SLOT;
+            }
+        }
+    }
+    // Above 256 buckets the GPU checks the declarations in a kernel before the
+    // crypt launch (include/zrc4.h): a disagreeing bucket's ids also block the
+    // groups they name, so every other bucket declaring one of them is refused
+    // too.  At most 256 buckets the groups travel in the kernel arguments and
+    // only the disagreeing bucket is refused.
+    if ((n + 255) / 256 > 256 && !lost.empty()) {
+        for (uint32_t b = 0; b < n; b += 256) {
+            if (std::find(lost.begin(), lost.end(), bg[b / 256]) == lost.end()) continue;
+            const uint32_t e = b + 256 < n ? b + 256 : n;
             for (uint32_t i = b; i < e; ++i) kept[i] = ZRC4_IDLE_SLOT;
         }
     }

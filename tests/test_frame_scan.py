@@ -16,6 +16,36 @@ import pyoracle
 BOUND = 20480
 
 
+
+def payload_report(got, want, off, ln):
+    """'' when the buffers match; else the count of differing bytes, the
+    first offsets and the sessions (entries) they fall in, with each one's
+    [off, off + len) span -- enough to tell a stray store from a wrong
+    keystream after one failing run (no reruns to reproduce)."""
+    bad = np.flatnonzero(got != want)
+    if bad.size == 0:
+        return ""
+    off = np.asarray(off, dtype=np.int64)
+    ln = np.asarray(ln, dtype=np.int64)
+    order = np.argsort(off, kind="stable")
+    ent = order[np.clip(np.searchsorted(off[order], bad[:16], side="right") - 1, 0, len(off) - 1)]
+    inside = (bad[:16] >= off[ent]) & (bad[:16] < off[ent] + ln[ent])
+    sess = sorted(set(int(e) for e in ent))
+    return (f"{bad.size} bytes differ; first offsets {bad[:16].tolist()}; entries {ent.tolist()} "
+            f"(inside their span: {inside.tolist()}); {len(np.unique(ent))} distinct among the first 16; "
+            f"spans {[(int(off[e]), int(off[e] + ln[e])) for e in sess[:4]]}; "
+            f"got {got[bad[:8]].tolist()} want {want[bad[:8]].tolist()}")
+
+
+def frame_report(w, g, name):
+    """'' when a framing output matches; else where it differs."""
+    w, g = np.asarray(w), np.asarray(g)
+    if np.array_equal(w, g):
+        return ""
+    rows = np.flatnonzero((w != g).reshape(len(w), -1).any(axis=1))
+    return (f"{name}: {rows.size} entries differ, first {rows[:8].tolist()}: "
+            f"want {w[rows[:4]].tolist()} got {g[rows[:4]].tolist()}")
+
 def pack_cases(frame_golden):
     cases = frame_golden["cases"]
     datas = [bytes.fromhex(c["data"]) for c in cases]
@@ -130,7 +160,8 @@ def test_device_scan_matches_oracle_at_baseline_shapes(built, n, avg, maxp):
     with Context(0, 256) as c:
         got = device_scan(torch, c, buf, off, ln, BOUND, maxp)
     for w, g, name in zip(want, got, ["npk", "used", "status", "pkt_len"]):
-        assert np.array_equal(w, g), name
+        msg = frame_report(w, g, name)
+        assert not msg, msg
 
 
 @pytest.mark.gpu
@@ -158,11 +189,13 @@ def test_decrypt_then_scan_pipeline(built):
         pk = torch.zeros(n * 8, dtype=torch.int32, device="cuda")
         c.frame_scan(d, d_off, d_len, BOUND, npk, used, status, pk, 8)
         c.sync()
-        assert np.array_equal(d.cpu().numpy(), buf)
+        msg = payload_report(d.cpu().numpy(), buf, off, ln)
+        assert not msg, msg
         got = (npk.cpu().numpy().view(np.uint32), used.cpu().numpy().view(np.uint32),
                status.cpu().numpy().view(np.uint32), pk.cpu().numpy().view(np.uint32).reshape(n, 8))
     for w, g, name in zip(want, got, ["npk", "used", "status", "pkt_len"]):
-        assert np.array_equal(w, g), name
+        msg = frame_report(w, g, name)
+        assert not msg, msg
 
 
 def _fused_case(n, avg, seed, tail_frac=0.5):
@@ -245,7 +278,8 @@ def test_fused_decrypt_and_frame(built, n, avg, mode):
             else:
                 c.crypt_grouped_frame(*args, frame)
         c.sync()
-        assert np.array_equal(d.cpu().numpy(), buf)
+        msg = payload_report(d.cpu().numpy(), buf, toff, tlen)
+        assert not msg, f"{mode} n={n}: {msg}"
         got = [npk.cpu().numpy().view(np.uint32), used.cpu().numpy().view(np.uint32),
                status.cpu().numpy().view(np.uint32), pk.cpu().numpy().view(np.uint32).reshape(-1, maxp)]
         if mode != "range":
@@ -255,4 +289,5 @@ def test_fused_decrypt_and_frame(built, n, avg, mode):
             perm[back[sel]] = np.flatnonzero(sel)
             got = [g[perm] for g in got]
     for w, g, name in zip(want, got, ["npk", "used", "status", "pkt_len"]):
-        assert np.array_equal(w, g), name
+        msg = frame_report(w, g, name)
+        assert not msg, f"{mode} n={n}: {msg}"

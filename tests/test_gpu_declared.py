@@ -205,3 +205,92 @@ def test_declared_argument_checks(built, torch_cuda):
         c.sync()
         ks = pyoracle.Rc4(b"").encryption(bytes(8))           # fresh slots: the empty-key state
         assert pay.cpu().numpy()[:8].tobytes() == ks
+
+
+def _claim_part(nb, cus, j):
+    """The part of a group a declared launch of nb buckets claims for group
+    lane j (zrc4_kernels.hpp Claim): the window kernel (nb <= 32) claims the
+    dword column q = col(j) >> 2, the half-group kernel (2 nb <= CUs) and the
+    persistent kernel (nb > CUs, wave-pair halves) the half j >> 7, the
+    whole-group kernel the whole group (part 0)."""
+    if nb <= 32:
+        return (j & 31) | ((j >> 7) << 5)
+    if 2 * nb <= cus or nb > cus:
+        return j >> 7
+    return 0
+
+
+@pytest.mark.parametrize("nb", [20, 100, 200, 700])
+def test_declared_two_buckets_one_group(built, torch_cuda, nb):
+    """two buckets of one declared launch both (correctly) declare
+    group A, with disjoint slots of it.  The claims (one per part of the
+    group, include/zrc4.h) let exactly one of the two buckets run each part:
+    every entry of the pair is crypted whole or not at all, no part has
+    crypted entries of both buckets, and ZRC4_ERR_GROUP is latched.  Above
+    256 buckets the declared check before the crypt passes both (they agree
+    with their declarations) and the persistent kernel's claims decide, per
+    wave-pair half.  Every other bucket, and every state, matches the
+    oracle."""
+    torch = torch_cuda
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rng = np.random.default_rng(1400 + nb)
+    G = max(256, nb + 40)
+    cap = 256 * G
+    c, ob, T = _seeded(torch, rng, cap)
+    s = torch.cuda.current_stream()
+    with c:
+        groups = rng.permutation(G)[:nb].astype(np.uint32)
+        A = int(groups[4])
+        groups[9] = A                                          # bucket 9 declares A too
+        ids = _buckets(rng, groups)
+        lanes = rng.permutation(256)
+        for b, half in ((4, lanes[:128]), (9, lanes[128:])):  # disjoint slots of A, spread over every part
+            ids[256 * b: 256 * (b + 1)] = IDLE_SLOT
+            ids[256 * b + rng.permutation(256)[:half.size]] = A * 256 + half
+        busy = ids != IDLE_SLOT
+        L = np.where(busy, rng.integers(8, 300, ids.size), 0).astype(np.uint32)
+        off = np.arange(ids.size, dtype=np.uint64) * 300
+        data = rng.integers(0, 256, ids.size * 300, dtype=np.uint8)
+        allc = _oracle_crypt(pyoracle_batch_copy(ob, cap), data, ids, off, L)   # every entry crypted
+        pay = T(data)
+        c.crypt_grouped_declared(pay, T(off.view(np.int64)), T(L.view(np.int32)), T(ids.view(np.int32)),
+                                 groups, stream=s)
+        with pytest.raises(ZRC4Error) as ei:
+            c.sync(s)
+        assert ei.value.code == -7                           # ZRC4_ERR_GROUP
+        got = pay.cpu().numpy()
+        ran = {}
+        for b in (4, 9):
+            for e in range(256 * b, 256 * (b + 1)):
+                if ids[e] == IDLE_SLOT:
+                    continue
+                a, z = int(off[e]), int(off[e] + L[e])
+                if np.array_equal(got[a:z], allc[a:z]):
+                    ran[e] = True
+                elif np.array_equal(got[a:z], data[a:z]):
+                    ran[e] = False
+                else:
+                    raise AssertionError(f"entry {e} (bucket {b}) half-crypted")
+        parts = {}
+        for e, r in ran.items():
+            if r:
+                parts.setdefault(_claim_part(nb, cus, int(ids[e]) & 255), set()).add(e // 256)
+        both = {p: bs for p, bs in parts.items() if len(bs) > 1}
+        assert not both, f"parts crypted by both buckets: {both}"
+        assert any(ran.values()), "one bucket runs each part it wins"
+        keep = ids.copy()
+        for e, r in ran.items():
+            if not r:
+                keep[e] = IDLE_SLOT
+        want = _oracle_crypt(ob, data, keep, off, L)
+        bad = np.flatnonzero(got != want)
+        assert bad.size == 0, (bad[:8], int(bad.size))
+        _check_states(c, ob, cap)
+
+
+def pyoracle_batch_copy(ob, cap):
+    """A second oracle batch with the same states (the all-crypted reference
+    must not advance the states the final check compares against)."""
+    cp = pyoracle.Batch(cap)
+    pyoracle.C.memmove(cp.st, ob.st, pyoracle.C.sizeof(ob.st))
+    return cp

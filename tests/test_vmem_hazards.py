@@ -37,16 +37,18 @@ PINNED = set(range(40, 104)) | set(range(148, 152)) | set(range(160, 224))
 PREFETCHING = ("crypt_stream_kernelILb1ELb0ELb0E", "crypt_stream_kernelILb1ELb1ELb0E",   # range / grouped
                "crypt_stream_kernelILb1ELb0ELb1E", "crypt_stream_kernelILb1ELb1ELb1E")   # framed
 WIN_GROUPED = ("crypt_win_kernelILi2E",)      # the window kernel's claim, issued from asm by lane 0 (r05)
+DECL = ("crypt_decl_kernel",)                 # the declared kernels' claim, lane 0 under an in-asm predicate (r06)
 
 
 def _check_one(item):
     name, insns = item
     dbg = {}
-    # the prefetching persistent kernels issue the grouped claim from asm
-    # with lane 0 alone: there every load is tracked, whatever the EXEC mask
-    # (ADVICE r04), so a compiler copy of the claim's register before its
-    # wait would be flagged too
-    partial = any(k in name for k in PREFETCHING + WIN_GROUPED)
+    # the prefetching persistent kernels, the grouped window kernels and the
+    # declared kernels issue the grouped claim from asm with lane 0 alone:
+    # there every load is tracked, whatever the EXEC mask,
+    # so a compiler copy of the claim's register before its wait would be
+    # flagged too
+    partial = any(k in name for k in PREFETCHING + WIN_GROUPED + DECL)
     hz, _ = vh.check_function(name, insns, debug=dbg, track_partial=partial, max_states=1500000)
     idx = {i.addr: i for i in insns}
     pinned = [a for a in dbg.get("loads", {}) if vh.vmem_dest(idx[a]) & PINNED]

@@ -102,6 +102,32 @@ __device__ __forceinline__ unsigned long long claim_part_async(const Claim &cl, 
     return old;
 }
 
+// claim_part_async under a wave-uniform predicate tested INSIDE the asm
+// (ADVICE r05): the statement runs on every path and defines its result on
+// every path (0 when the predicate is false), so the compiler has no phi to
+// merge it through -- a merge copy of a register whose atomic is still in
+// flight would read it before claim_wait.
+__device__ __forceinline__ unsigned long long claim_part_async_if(const Claim &cl, uint32_t g, uint32_t part,
+                                                                  uint32_t bucket, uint32_t pred)
+{
+    unsigned long long old;
+    uint64_t sv;
+    const unsigned long long v = ((unsigned long long)cl.epoch << 32) | bucket;
+    unsigned long long *addr = cl.word + (size_t)g * kClaimParts + part;
+    asm volatile("v_mov_b64 %[old], 0\n\t"
+                 "s_cmp_eq_u32 %[p], 0\n\t"
+                 "s_cbranch_scc1 CLAIM_SKIP_%=\n\t"
+                 "s_mov_b64 %[sv], exec\n\t"
+                 "s_mov_b64 exec, 1\n\t"
+                 "global_atomic_swap_x2 %[old], %[a], %[v], off sc0\n\t"
+                 "s_mov_b64 exec, %[sv]\n\t"
+                 "CLAIM_SKIP_%=:"
+                 : [old] "=&v"(old), [sv] "=&s"(sv)
+                 : [a] "v"(addr), [v] "v"(v), [p] "s"(__builtin_amdgcn_readfirstlane(pred))
+                 : "memory", "scc");
+    return old;
+}
+
 // Retire every VMEM op in flight, claim_part_async's answer included.
 __device__ __forceinline__ void claim_wait(unsigned long long &old)
 {
@@ -1439,8 +1465,11 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
                                    xy + gl * 256u + j, arena + (size_t)gl * kGroupBytes, vo0);
             }
             xyd = (uint16_t)xv;
-            if (gdecl != ZRC4_INVALID && __builtin_amdgcn_readfirstlane(tid >> 6) == 0u)
-                coldd = claim_part_async(cl, gdecl, HALF ? h : 0u, w);   // thread 0 (lane 0 of wave 0)
+            // thread 0 (lane 0 of wave 0) claims; the predicate is wave-uniform
+            // and tested inside the asm, which every wave runs (no merge)
+            coldd = claim_part_async_if(cl, gl, HALF ? h : 0u, w,
+                                        (gdecl != ZRC4_INVALID && __builtin_amdgcn_readfirstlane(tid >> 6) == 0u)
+                                            ? 1u : 0u);
         }
 #pragma unroll
         for (uint32_t q = 0; q < kPer; ++q) {
@@ -1517,7 +1546,9 @@ crypt_body(uint8_t *__restrict__ arena, uint16_t *__restrict__ xy,
             if constexpr (DECL)                          // (no load left in flight at exit)
                 asm volatile("s_waitcnt vmcnt(0)" : "+{v[160:191]}"(ilo), "+{v[192:223]}"(ihi) :: "memory");
             if constexpr (FRAME) {                       // an idle bucket still reports its framing
-                if (valid && gmin == 0xFFFFFFFFu)
+                // (a refused one writes nothing: a bucket declared idle that
+                // holds a busy entry has gmin == INVALID and dup set)
+                if (valid && gmin == 0xFFFFFFFFu && !dup)
                     frame_walk(payload + fr.off[e], fr.len[e], fr.bound, fr.maxp, e, fr.npk, fr.used, fr.status,
                                fr.pkt_len);
             }
