@@ -542,6 +542,56 @@ def host_inclusive(args):
     per = -(-per // 256) * 256                      # whole 256-slot groups per chunk
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
     times = []
+    if getattr(args, "ids", "range") != "range" and args.zero_copy:
+        # The session engine's own path: its receive / send blocks live in a
+        # pinned SessionBlock pool, and each event-loop iteration runs ONE
+        # zrc4_crypt_grouped_declared over them in place (buckets built and
+        # declared on the host; device ids / offsets / lengths).  Slots in
+        # random order inside each group, groups in random order.
+        if S % 256:
+            raise SystemExit("--ids declared --zero-copy needs whole groups")
+        rng = np.random.default_rng(77)
+        order = rng.permutation(S // 256)
+        ids = np.concatenate([g * 256 + rng.permutation(256) for g in order]).astype(np.uint32)
+        d_ids = T(ids.view(np.int32))
+        d_off = T((ids.astype(np.int64) * L))
+        d_len = T(np.full(S, L, dtype=np.int32))
+        groups = order.astype(np.uint32)
+        st = streams[0]
+        for it in range(args.warmup + args.steps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ctx.crypt_grouped_declared(host, d_off, d_len, d_ids, groups, stream=st)
+            torch.cuda.synchronize()
+            if it >= args.warmup:
+                times.append(time.perf_counter() - t0)
+        ctx.sync(st)
+        t = statistics.median(times)
+        return {"metric": "RC4 GiB/s host-inclusive (engine path: zrc4_crypt_grouped_declared on pinned host blocks)",
+                "value": round(S * L / t / GIB, 3), "unit": "GiB/s", "ms_per_pass": round(t * 1e3, 4),
+                "workload": args.workload, "ids": "declared buckets, random slot and group order",
+                "pcie_bytes_per_pass": 2 * S * L, "note": "not the headline value (DESIGN.md)"}
+    if getattr(args, "ids", "range") != "range":
+        # The engine's shape through the host-pointer C-ABI: zrc4_crypt_host
+        # with the sessions' slot ids in random order; the library buckets
+        # them by group on the host, declares each bucket's group
+        # (zrc4_crypt_grouped_declared) and moves the payload through its
+        # pinned staging (zero-copy up to 256 KiB, device copies above).
+        rng = np.random.default_rng(77)
+        ids = rng.permutation(S).astype(np.uint32)
+        hoff = (ids.astype(np.uint64) * L)
+        hlen = np.full(S, L, dtype=np.uint32)
+        buf = w.payload.copy()
+        for it in range(args.warmup + args.steps):
+            t0 = time.perf_counter()
+            ctx.crypt_host(buf, hoff, hlen, ids=ids)
+            if it >= args.warmup:
+                times.append(time.perf_counter() - t0)
+        t = statistics.median(times)
+        return {"metric": "RC4 GiB/s host-inclusive (zrc4_crypt_host: host ids bucketed and declared by the library)",
+                "value": round(S * L / t / GIB, 3), "unit": "GiB/s", "ms_per_pass": round(t * 1e3, 4),
+                "workload": args.workload, "ids": "random slot order, bucketed on the host",
+                "pcie_bytes_per_pass": 2 * S * L, "note": "not the headline value (DESIGN.md)"}
     if args.zero_copy:
         # the kernels read and write the pinned host buffer in place over PCIe
         # (the session engine's pinned SessionBlock pool does the same)

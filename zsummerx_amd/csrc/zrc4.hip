@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <vector>
 #include <new>
+#include <thread>
 
 #ifndef ZRC4_HALF
 #define ZRC4_HALF 1   // A/B knob: 0 runs few-group range batches on whole-group workgroups too
@@ -567,6 +568,37 @@ int zrc4_ksa_host(zrc4_ctx *c, const uint32_t *ids, const uint8_t *keys, size_t 
     return check_err(c, c->stream);
 }
 
+// Payload staging copies of the *_host calls (caller memory <-> pinned
+// staging): one host thread moves ~8 GB/s, so copies of 2 MiB and more are
+// split over up to 8 threads (r06: 512 MiB took ~67 ms on one thread).  If
+// a thread cannot be started, its share is copied on the calling thread.
+static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n)
+{
+    constexpr size_t kPerThreadMin = 1u << 20;
+    size_t nt = n / kPerThreadMin;
+    const unsigned hw = std::thread::hardware_concurrency();
+    if (nt > 8) nt = 8;
+    if (hw && nt > hw) nt = hw;
+    if (nt <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t per = ((n + nt - 1) / nt + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    size_t started = 1;                     // chunk 0 is this thread's
+    try {
+        th.reserve(nt - 1);
+        for (; started < nt && started * per < n; ++started) {
+            const size_t a = started * per, len = std::min(per, n - a);
+            th.emplace_back([=] { memcpy(dst + a, src + a, len); });
+        }
+    } catch (...) {
+    }
+    memcpy(dst, src, std::min(per, n));
+    for (size_t t = started; t * per < n; ++t) memcpy(dst + t * per, src + t * per, std::min(per, n - t * per));
+    for (auto &t : th) t.join();
+}
+
 int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t payload_bytes,
                     const uint64_t *off, const uint32_t *len, uint32_t n)
 {
@@ -585,20 +617,29 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
     // zrc4_crypt_grouped contract), so every group's S-boxes move as one
     // coalesced image instead of 256 strided byte accesses per slot.  A slot
     // may appear once per call (as for every batched entry point).
+    // Bucketing is one counting pass over the groups (r06; a comparison sort
+    // of the ids cost 91 ms at 524 288 entries, more than the copies): bucket
+    // b = the b-th group with entries, in ascending group order, its entries in
+    // call order; a 256-bit mask per group finds a repeated slot.
     const bool grouped = ids && n > 1;
-    std::vector<uint32_t> order, bgroup;     // bgroup: each bucket's group, declared to the kernel
+    std::vector<uint32_t> bgroup, bstart;     // bgroup: each bucket's group, declared to the kernel
     uint32_t buckets = 0;
     if (grouped) {
-        order.resize(n);
-        for (uint32_t i = 0; i < n; ++i) order[i] = i;
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ids[a] < ids[b]; });
-        for (uint32_t k = 0; k < n; ++k) {
-            if (k && ids[order[k]] == ids[order[k - 1]]) return ZRC4_ERR_INVALID_ARG;
-            if (!k || (ids[order[k]] >> 8) != (ids[order[k - 1]] >> 8)) {
-                ++buckets;
-                bgroup.push_back(ids[order[k]] >> 8);
-            }
+        const uint32_t ngroups = c->capacity / zrc4::kGroup;
+        std::vector<uint64_t> seen((size_t)ngroups * 4, 0);
+        bstart.assign(ngroups, ZRC4_IDLE_SLOT);
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t g = ids[i] >> 8, k = ids[i] & 255u;
+            uint64_t &w = seen[(size_t)g * 4 + (k >> 6)];
+            if (w >> (k & 63u) & 1u) return ZRC4_ERR_INVALID_ARG;
+            w |= 1ull << (k & 63u);
+            bstart[g] = 0;
         }
+        for (uint32_t g = 0; g < ngroups; ++g)
+            if (bstart[g] != ZRC4_IDLE_SLOT) {
+                bstart[g] = buckets++ * zrc4::kGroup;
+                bgroup.push_back(g);
+            }
     }
     const uint32_t m = grouped ? buckets * zrc4::kGroup : n;      // entries the kernel sees
     const size_t o_ids = 0, s_ids = ids ? align16((size_t)m * 4) : 0;
@@ -615,14 +656,8 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
             bo[e] = 0;
             bl[e] = 0;
         }
-        uint32_t b = 0, pos = 0;
-        for (uint32_t k = 0; k < n; ++k) {
-            const uint32_t i = order[k];
-            if (k && (ids[i] >> 8) != (ids[order[k - 1]] >> 8)) {
-                ++b;
-                pos = 0;
-            }
-            const uint32_t e = b * zrc4::kGroup + pos++;
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t e = bstart[ids[i] >> 8]++;     // (at most 256 per group: no slot twice)
             bi[e] = ids[i];
             bo[e] = off[i];
             bl[e] = len[i];
@@ -632,7 +667,7 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
         memcpy(c->h_stage + o_off, off, (size_t)n * 8);
         memcpy(c->h_stage + o_len, len, (size_t)n * 4);
     }
-    if (payload_bytes) memcpy(c->h_stage + o_pay, payload, payload_bytes);
+    if (payload_bytes) par_memcpy(c->h_stage + o_pay, payload, payload_bytes);
     // Small batches (the per-call RC4Encryption::encryption drop-in) run on
     // the pinned staging copy in place: no H2D / D2H copies on the latency
     // path.  Large ones are copied so the kernel streams HBM, not PCIe.
@@ -652,7 +687,7 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
                                 hipMemcpyDeviceToHost, c->stream));
     rc = check_err(c, c->stream);
     if (rc) return rc;
-    if (payload_bytes) memcpy(payload, c->h_stage + o_pay, payload_bytes);
+    if (payload_bytes) par_memcpy(payload, c->h_stage + o_pay, payload_bytes);
     return ZRC4_OK;
 }
 
