@@ -205,3 +205,70 @@ def test_reference_batch_matches_the_restatement():
                                  int(w.length[i]))
     ob.crypt(p2, w.off, w.length)
     assert np.array_equal(p1, p2)
+
+
+class _ShardRunner:
+    """bench.GpuRunner's interface for shard_projection, on the CPU: every
+    launch records (first_slot, n) and 'takes' n * 1e-6 ms, so a shard of
+    S/N sessions times N times faster than the whole batch."""
+    class _Fn:
+        __name__ = "zrc4_crypt_range"
+
+        def __init__(self, log):
+            self.log = log
+
+        def __call__(self, h, first, pay, offp, lenp, n, st):
+            self.log.append((first, offp.value, lenp.value, n))
+            return 0
+
+    def __init__(self, S, L):
+        import ctypes as C
+        self.S, self.L, self.R, self.log = S, L, 1, []
+        self._fn = self._Fn(self.log)
+        self._args = [(None, 0, C.c_void_p(1 << 20), C.c_void_p(2 << 20), C.c_void_p(3 << 20), S, None)]
+
+    def step(self, i):
+        self._fn(*self._args[i % self.R])
+
+    def sync(self):
+        pass
+
+    def check(self):
+        pass
+
+    def make_events(self, k, every=16):
+        return [None] * (-(-k // every) + 1)
+
+    def launch_steps(self, first, k, every, marks):
+        for seg, d in enumerate(range(0, k, every)):
+            m = min(every, k - d)
+            for i in range(first + d, first + d + m):
+                self.step(i)
+            marks[seg] = self._args[0][5] * 1e-6       # ms per launch, proportional to the shard
+
+    @staticmethod
+    def segment_ms(k, every, marks):
+        return [v for v in marks if v is not None]
+
+
+def test_shard_projection_splits_the_batch_into_contiguous_shards():
+    """configs4_strong.shard_projection (N = 1 only): shard k of N is slots
+    [k S/N, (k+1) S/N) with its offsets / lengths advanced to match, the
+    shards rotate, the runner is restored afterwards, and the speed-ups are
+    the 1-GPU kernel time over each shard's."""
+    import argparse
+    import bench
+    S, L = 524288, 1024
+    run = _ShardRunner(S, L)
+    saved = list(run._args)
+    c = argparse.Namespace(workload="cfg5", warmup=2, steps=32, event_every=16)
+    res = {"roofline": {"kernel_avg_us": S * 1e-3}, "ms_per_step": S * 1e-6}
+    proj = bench.shard_projection(c, run, res)
+    assert [s["gpus"] for s in proj["shards"]] == [2, 4, 8]
+    for s in proj["shards"]:
+        n = s["gpus"]
+        assert s["sessions_per_gpu"] == S // n
+        assert abs(s["projected_speedup_kernel"] - n) < 1e-6
+    assert run._args == saved and run.R == 1
+    shards8 = {(f, o, ln, n) for f, o, ln, n in run.log if n == S // 8}
+    assert shards8 == {(k * S // 8, (2 << 20) + 8 * k * S // 8, (3 << 20) + 4 * k * S // 8, S // 8) for k in range(8)}
