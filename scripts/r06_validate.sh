@@ -15,6 +15,10 @@ step() {  # name, seconds, command...
     echo "[$name] rc=$rc"; grep -v amdgpu.ids "$OUT/$name.log" | tail -${TAILN:-2} | cut -c1-600
     if [ $rc -ne 0 ]; then echo "[$name] failed: stopping GPU work in this call"; exit $rc; fi
 }
+# VAL_PHASE=bench: tests, smoke and bench lines; VAL_PHASE=prof: rocprofv3
+# kernel stats and PMC traffic only (two calls: each fits gpurun's limit)
+PHASE=${VAL_PHASE:-all}
+if [ "$PHASE" != prof ]; then
 if [ -z "${VAL_SKIP_TESTS:-}" ]; then
   TAILN=4 step gpu_tests 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider
   step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
@@ -29,6 +33,8 @@ step bench_cfg5_grouped 300 python bench.py --workload cfg5 --ids grouped --step
 step bench_cfg3 200 python bench.py --workload cfg3 --steps 200 --warmup 20 --cpu-seconds 0
 step bench_cfg3_declared 200 python bench.py --workload cfg3 --ids declared --steps 200 --warmup 20 --cpu-seconds 0
 step bench_cfg4 200 python bench.py --workload cfg4 --steps 50 --warmup 5 --cpu-seconds 0
+[ "$PHASE" = bench ] && { echo "bench phase done"; exit 0; }
+fi
 cd /tmp && export TMPDIR=/tmp
 for wl in cfg2 cfg3 cfg4 cfg5 cfg5-grouped cfg2-grouped cfg2-declared cfg3-declared; do
   W=20; [ ${wl%%-*} = cfg5 ] && W=120
