@@ -211,6 +211,48 @@ def test_crypt_host_scattered_ids_grouped(built, torch_cuda):
             assert c.get_state(int(bid[2])) == before and not buf.any()
 
 
+@pytest.mark.parametrize("ids_mode", ["range", "ids"])
+def test_crypt_host_large_batch_pipelined(built, torch_cuda, ids_mode):
+    """zrc4_crypt_host above 32 MiB of payload moves it in 16 MiB chunks
+    (host copy of chunk k+1 overlapping the DMA of chunk k, both ways) and
+    buckets ids by a counting pass (r06): 45 000 sessions of 0-1 800 bytes
+    (~40 MiB, a ragged last chunk), ids in random order, two calls, against
+    the oracle; states of a sample of slots checked too."""
+    rng = np.random.default_rng(321)
+    n, cap = 45000, 65536
+    ids = rng.permutation(cap)[:n].astype(np.uint32) if ids_mode == "ids" else None
+    slots = ids if ids is not None else np.arange(n, dtype=np.uint32)
+    keys = rng.integers(0, 256, 16 * n, dtype=np.uint8)
+    ob = pyoracle.Batch(cap)
+    koff = np.zeros(cap, dtype=np.uint64)
+    klen = np.zeros(cap, dtype=np.uint32)
+    koff[slots] = np.arange(n, dtype=np.uint64) * 16
+    klen[slots] = 16
+    ob.make_sbox(keys, koff, klen)
+    L = rng.integers(0, 1800, n).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(L[:-1] + 1)]).astype(np.uint64)
+    data = rng.integers(0, 256, int(off[-1] + L[-1]) + 5, dtype=np.uint8)
+    assert data.nbytes > 32 << 20
+    with Context(0, cap) as c:
+        c.ksa_host([keys[16 * i:16 * i + 16].tobytes() for i in range(n)], ids=slots)
+        for call in range(2):
+            want = data.copy()
+            sl_off = np.zeros(cap, dtype=np.uint64)
+            sl_len = np.zeros(cap, dtype=np.uint32)
+            sl_off[slots] = off
+            sl_len[slots] = L
+            ob.crypt(want, sl_off, sl_len, threads=8)
+            got = data.copy()
+            c.crypt_host(got, off, L, ids=ids)
+            bad = np.flatnonzero(got != want)
+            assert bad.size == 0, (call, bad[:8].tolist(), int(bad.size))
+            data = got
+        for s in slots[rng.permutation(n)[:64]]:
+            sb, x, y = c.get_state(int(s))
+            osb, ox, oy = ob.state(int(s))
+            assert (bytes(sb), x, y) == (bytes(osb), ox, oy), int(s)
+
+
 def test_batch_whole_group_ids(ctx, batch_small):
     """ids given but exactly an aligned 256-slot group -> coalesced fast path."""
     rng = np.random.default_rng(9)

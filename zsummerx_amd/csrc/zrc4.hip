@@ -599,6 +599,52 @@ static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n)
     for (auto &t : th) t.join();
 }
 
+// The chunked D2H of a piped zrc4_crypt_host: chunk k's copy is recorded
+// with an event and copied out to the caller once it has landed, while the
+// later chunks are still in flight.  The kernel ran before the first chunk's
+// copy, so the fault latch is final once that chunk has landed: on a fault
+// nothing is copied out (as on the unpiped path).  Without events (creation
+// failed) it waits for the stream and copies everything at once.
+static constexpr size_t kPipeChunk = 16u << 20;
+
+static int copy_back_piped(zrc4_ctx *c, uint8_t *payload, size_t o_pay, size_t payload_bytes)
+{
+    std::vector<hipEvent_t> ev;
+    ev.reserve(payload_bytes / kPipeChunk + 1);
+    bool evs = true;
+    for (size_t a = 0; a < payload_bytes; a += kPipeChunk) {
+        const size_t l = std::min(kPipeChunk, payload_bytes - a);
+        hipError_t e = hipMemcpyAsync(c->h_stage + o_pay + a, c->d_stage + o_pay + a, l, hipMemcpyDeviceToHost,
+                                      c->stream);
+        if (e != hipSuccess) evs = false;
+        hipEvent_t x = nullptr;
+        if (evs && hipEventCreateWithFlags(&x, hipEventDisableTiming) == hipSuccess) {
+            if (hipEventRecord(x, c->stream) == hipSuccess) {
+                ev.push_back(x);
+                continue;
+            }
+            (void)hipEventDestroy(x);
+        }
+        evs = false;
+    }
+    int rc = ZRC4_OK;
+    if (!evs || ev.empty() || hipEventSynchronize(ev[0]) != hipSuccess) {
+        rc = check_err(c, c->stream);
+        if (rc == ZRC4_OK) par_memcpy(payload, c->h_stage + o_pay, payload_bytes);
+    } else if ((rc = read_faults(c)) == ZRC4_OK) {
+        for (size_t k = 0, a = 0; a < payload_bytes; ++k, a += kPipeChunk) {
+            if (hipEventSynchronize(ev[k]) != hipSuccess) {
+                rc = ZRC4_ERR_HIP;
+                break;
+            }
+            par_memcpy(payload + a, c->h_stage + o_pay + a, std::min(kPipeChunk, payload_bytes - a));
+        }
+    }
+    (void)hipStreamSynchronize(c->stream);
+    for (hipEvent_t x : ev) (void)hipEventDestroy(x);
+    return rc;
+}
+
 int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t payload_bytes,
                     const uint64_t *off, const uint32_t *len, uint32_t n)
 {
@@ -667,21 +713,37 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
         memcpy(c->h_stage + o_off, off, (size_t)n * 8);
         memcpy(c->h_stage + o_len, len, (size_t)n * 4);
     }
-    if (payload_bytes) par_memcpy(c->h_stage + o_pay, payload, payload_bytes);
     // Small batches (the per-call RC4Encryption::encryption drop-in) run on
     // the pinned staging copy in place: no H2D / D2H copies on the latency
-    // path.  Large ones are copied so the kernel streams HBM, not PCIe.
+    // path.  Large ones are copied so the kernel streams HBM, not PCIe; from
+    // 2 chunks of kPipeChunk on, the payload moves chunk by chunk so each
+    // chunk's host copy overlaps the previous chunk's DMA (and, on the way
+    // back, the next chunk's DMA overlaps this chunk's host copy).
     const bool zero_copy = total <= kZeroCopyMax;
+    const bool piped = !zero_copy && payload_bytes >= 2 * kPipeChunk;
     uint8_t *st = c->h_stage;
-    if (!zero_copy) {
-        ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
+    if (piped) {
+        ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, o_pay, hipMemcpyHostToDevice, c->stream));
+        for (size_t a = 0; a < payload_bytes; a += kPipeChunk) {
+            const size_t l = std::min(kPipeChunk, payload_bytes - a);
+            par_memcpy(c->h_stage + o_pay + a, payload + a, l);
+            ZRC4_TRY(hipMemcpyAsync(c->d_stage + o_pay + a, c->h_stage + o_pay + a, l, hipMemcpyHostToDevice,
+                                    c->stream));
+        }
         st = c->d_stage;
+    } else {
+        if (payload_bytes) par_memcpy(c->h_stage + o_pay, payload, payload_bytes);
+        if (!zero_copy) {
+            ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
+            st = c->d_stage;
+        }
     }
     rc = launch_crypt(c, grouped ? zrc4::kGrouped : ids ? zrc4::kIds : zrc4::kRange,
                       ids ? (const uint32_t *)(st + o_ids) : nullptr, 0, st + o_pay, (const uint64_t *)(st + o_off),
                       (const uint32_t *)(st + o_len), m, c->stream, nullptr, grouped ? bgroup.data() : nullptr,
                       true);
     if (rc) return rc;
+    if (piped) return copy_back_piped(c, payload, o_pay, payload_bytes);
     if (payload_bytes && !zero_copy)
         ZRC4_TRY(hipMemcpyAsync(c->h_stage + o_pay, c->d_stage + o_pay, payload_bytes,
                                 hipMemcpyDeviceToHost, c->stream));
