@@ -37,6 +37,20 @@ def run(exe, *args, env=None):
     return out
 
 
+def test_emulated_declared_refusals_match_the_gpu_rules(tools):
+    """the CPU emulation the engine tests run on refuses declared
+    buckets as the GPU does -- at most 256 buckets only the bucket whose ids
+    leave its declared group; above 256 also the bucket that legitimately
+    declares a group those ids name (the declared-check kernel's blocking,
+    include/zrc4.h).  GPU side: test_gpu_declared.py."""
+    exe = tools / "emu_declared_check"
+    if not exe.exists():                               # sanitizer tool dirs build only the engine binaries
+        pytest.skip("emu_declared_check not in this tools dir")
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert p.stdout.count("-> ok") == 5, p.stdout
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_reservoir_host_logic_emulated(tools, seed):
     run(tools / "hooks_check_emu", "device", 48, 150, seed)

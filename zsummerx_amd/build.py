@@ -146,6 +146,8 @@ def build_test_tools(force: bool = False, sanitize: bool | str = False) -> Path:
       tools/bin/hooks_check_emu  the same host logic over a CPU emulation of
                                  the zrc4 C-ABI (tests/cpp/emu_zrc4_hip.cpp)
       tools/bin/frame_stress_emu the engine + device hooks over that emulation
+      tools/bin/emu_declared_check  the emulation's declared-group refusals
+                                 against the GPU's rules
     sanitize=True builds only the two emulated binaries, with ASan + UBSan,
     into tools/bin/san/ (scripts/sanitize.sh runs the CPU suites on them);
     sanitize="thread" the same with ThreadSanitizer into tools/bin/tsan/ (the
@@ -169,6 +171,9 @@ def build_test_tools(force: bool = False, sanitize: bool | str = False) -> Path:
         (out / "hooks_check_emu", [chk, orc, emu] + FRAME_DEPS,
          ["g++", "-O2", *common, *emu_flags, "-o", str(out / "hooks_check_emu"), str(chk), str(dev), str(emu),
           *oracle_link, "-lpthread"]),
+        (out / "emu_declared_check", [orc, emu, ROOT / "tests" / "cpp" / "emu_declared_check.cpp", ROOT / "include" / "zrc4.h"],
+         ["g++", "-O2", *common, *emu_flags, "-o", str(out / "emu_declared_check"),
+          str(ROOT / "tests" / "cpp" / "emu_declared_check.cpp"), str(emu), *oracle_link, "-lpthread"]),
         (out / "frame_stress_emu", [orc, emu, ROOT / "tools" / "frame_stress.cpp"] + FRAME_DEPS,
          ["g++", "-O2", *common, *emu_flags, "-o", str(out / "frame_stress_emu"), str(ROOT / "tools" / "frame_stress.cpp"),
           *map(str, FRAME_SOURCES), str(emu), *oracle_link, "-ldl", "-lpthread"]),
