@@ -611,12 +611,12 @@ static int copy_back_piped(zrc4_ctx *c, uint8_t *payload, size_t o_pay, size_t p
 {
     std::vector<hipEvent_t> ev;
     ev.reserve(payload_bytes / kPipeChunk + 1);
-    bool evs = true;
+    bool evs = true, copies = true;
     for (size_t a = 0; a < payload_bytes; a += kPipeChunk) {
         const size_t l = std::min(kPipeChunk, payload_bytes - a);
         hipError_t e = hipMemcpyAsync(c->h_stage + o_pay + a, c->d_stage + o_pay + a, l, hipMemcpyDeviceToHost,
                                       c->stream);
-        if (e != hipSuccess) evs = false;
+        if (e != hipSuccess) copies = evs = false;
         hipEvent_t x = nullptr;
         if (evs && hipEventCreateWithFlags(&x, hipEventDisableTiming) == hipSuccess) {
             if (hipEventRecord(x, c->stream) == hipSuccess) {
@@ -628,7 +628,10 @@ static int copy_back_piped(zrc4_ctx *c, uint8_t *payload, size_t o_pay, size_t p
         evs = false;
     }
     int rc = ZRC4_OK;
-    if (!evs || ev.empty() || hipEventSynchronize(ev[0]) != hipSuccess) {
+    if (!copies) {                         // a chunk never left the device: copy nothing out
+        rc = check_err(c, c->stream);
+        if (rc == ZRC4_OK) rc = ZRC4_ERR_HIP;
+    } else if (!evs || ev.empty() || hipEventSynchronize(ev[0]) != hipSuccess) {
         rc = check_err(c, c->stream);
         if (rc == ZRC4_OK) par_memcpy(payload, c->h_stage + o_pay, payload_bytes);
     } else if ((rc = read_faults(c)) == ZRC4_OK) {
