@@ -726,12 +726,18 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
     const bool piped = !zero_copy && payload_bytes >= 2 * kPipeChunk;
     uint8_t *st = c->h_stage;
     if (piped) {
-        ZRC4_TRY(hipMemcpyAsync(c->d_stage, c->h_stage, o_pay, hipMemcpyHostToDevice, c->stream));
-        for (size_t a = 0; a < payload_bytes; a += kPipeChunk) {
+        // (a failed enqueue returns only once the chunks already queued have
+        // left the staging buffer, which the next call rewrites)
+        bool ok = hipMemcpyAsync(c->d_stage, c->h_stage, o_pay, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+        for (size_t a = 0; ok && a < payload_bytes; a += kPipeChunk) {
             const size_t l = std::min(kPipeChunk, payload_bytes - a);
             par_memcpy(c->h_stage + o_pay + a, payload + a, l);
-            ZRC4_TRY(hipMemcpyAsync(c->d_stage + o_pay + a, c->h_stage + o_pay + a, l, hipMemcpyHostToDevice,
-                                    c->stream));
+            ok = hipMemcpyAsync(c->d_stage + o_pay + a, c->h_stage + o_pay + a, l, hipMemcpyHostToDevice,
+                                c->stream) == hipSuccess;
+        }
+        if (!ok) {
+            (void)hipStreamSynchronize(c->stream);
+            return ZRC4_ERR_HIP;
         }
         st = c->d_stage;
     } else {
@@ -745,7 +751,10 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
                       ids ? (const uint32_t *)(st + o_ids) : nullptr, 0, st + o_pay, (const uint64_t *)(st + o_off),
                       (const uint32_t *)(st + o_len), m, c->stream, nullptr, grouped ? bgroup.data() : nullptr,
                       true);
-    if (rc) return rc;
+    if (rc) {
+        if (piped) (void)hipStreamSynchronize(c->stream);
+        return rc;
+    }
     if (piped) return copy_back_piped(c, payload, o_pay, payload_bytes);
     if (payload_bytes && !zero_copy)
         ZRC4_TRY(hipMemcpyAsync(c->h_stage + o_pay, c->d_stage + o_pay, payload_bytes,
