@@ -218,13 +218,15 @@ def _fused_case(n, avg, seed, tail_frac=0.5):
 @pytest.mark.parametrize("n,avg,mode", [(4096, 900, "range"), (1000, 3000, "grouped"), (70000, 200, "range"),
                                         (150000, 200, "grouped"), (600000, 40, "range"), (600000, 40, "grouped"),
                                         (1000, 3000, "declared"), (25000, 300, "declared"), (40000, 300, "declared"),
-                                        (150000, 200, "declared")])
+                                        (150000, 200, "declared"), (600001, 40, "range"), (333333, 48, "range")])
 def test_fused_decrypt_and_frame(built, n, avg, mode):
     """zrc4_crypt_*_frame: decrypt the fresh tail and frame the WHOLE block in
     one launch: the direct kernels' epilogue at <= 1 group per CU, the
     persistent kernel's tail above (70 000 / 150 000 sessions: 274 / 587
     groups, one or two chunks per workgroup; 600 000: 2 344 groups, five
-    chunks per workgroup, the tail's four-walk lockstep plus a remainder).
+    chunks per workgroup, the tail's four-walk lockstep plus a remainder;
+    r06: 600 001 -- the round-5 red shape with other inputs and a last group
+    of one session -- and 333 333, 1 303 groups with a 21-session tail).
     declared: zrc4_crypt_grouped_declared with framing, the engine's call --
     6 buckets on the window kernel, ~100 and ~159 on crypt_decl_kernel
     (half- and whole-group), ~587 behind the declared check on the
