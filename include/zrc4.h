@@ -234,8 +234,13 @@ int zrc4_frame_scan(zrc4_ctx *ctx, const uint8_t *buf, const uint64_t *off,
  * size: in the chain-bound regime (at most one slot group per CU) each lane
  * frames its own session in the crypt kernel's epilogue; larger batches run
  * the persistent throughput kernel, whose workgroups frame the entries of the
- * 256-entry chunks they decrypted in their tail.  Outputs of a bucket refused
- * with ZRC4_ERR_GROUP are unspecified.  Device pointers; asynchronous. */
+ * 256-entry chunks they decrypted in their tail.  Framing outputs of a bucket
+ * refused with ZRC4_ERR_GROUP are unspecified, with one guarantee on launches
+ * of at most one bucket per CU (the window, half- and whole-group kernels,
+ * declared or not): its busy entries (the ones it would have decrypted) are
+ * never framed over their undecrypted bytes.  (The persistent kernel's tail
+ * walks every chunk, a refused bucket's included, on its bytes as they
+ * stand.)  Device pointers; asynchronous. */
 typedef struct zrc4_frame_args {
     const uint64_t *off;
     const uint32_t *len;

@@ -294,3 +294,72 @@ def pyoracle_batch_copy(ob, cap):
     cp = pyoracle.Batch(cap)
     pyoracle.C.memmove(cp.st, ob.st, pyoracle.C.sizeof(ob.st))
     return cp
+
+
+@pytest.mark.parametrize("nb", [20, 100, 200, 700])
+def test_declared_refused_bucket_frames_nothing(built, torch_cuda, nb):
+    """with framing, a refused declared bucket decrypts nothing
+    and never frames a busy entry over its undecrypted bytes, whether it is
+    refused for ids outside its declared group (bucket 2) or for a busy
+    entry in a bucket declared idle (bucket 5; on the declared kernels that
+    one reached the idle-bucket branch, which framed every entry).  The rest
+    of a refused bucket's framing outputs is unspecified (include/zrc4.h).
+    Every other entry, idle ones included, is framed as the oracle frames
+    the expected buffer.  700 buckets run the persistent kernel, whose tail
+    walks every chunk: there only the other buckets are checked."""
+    torch = torch_cuda
+    rng = np.random.default_rng(1500 + nb)
+    G = max(256, nb + 40)
+    cap = 256 * G
+    c, ob, T = _seeded(torch, rng, cap)
+    s = torch.cuda.current_stream()
+    with c:
+        perm = rng.permutation(G)
+        groups = perm[:nb].astype(np.uint32)
+        H, H2 = int(perm[nb]), int(perm[nb + 1])
+        ids = _buckets(rng, groups)
+        ids[256 * 2: 256 * 3] = IDLE_SLOT
+        ids[256 * 2 + rng.permutation(256)[:50]] = H * 256 + rng.permutation(256)[:50]
+        groups[5] = IDLE_SLOT
+        ids[256 * 5: 256 * 6] = IDLE_SLOT
+        ids[256 * 5 + 9] = H2 * 256 + 3
+        groups[11] = IDLE_SLOT                            # a genuinely idle bucket: framed raw
+        ids[256 * 11: 256 * 12] = IDLE_SLOT
+        busy = ids != IDLE_SLOT
+        L = np.where(busy, rng.integers(1, 400, ids.size), rng.integers(0, 40, ids.size)).astype(np.uint32)
+        off = np.arange(ids.size, dtype=np.uint64) * 400
+        data = rng.integers(0, 256, ids.size * 400, dtype=np.uint8)
+        # proto4z-looking headers at the span starts, so walks go past the first packet
+        for e in range(0, ids.size, 3):
+            data[int(off[e]): int(off[e]) + 4] = np.frombuffer(int(rng.integers(6, 120)).to_bytes(4, "little"), np.uint8)
+        want = _oracle_crypt(ob, data, ids, off, L, skip=(H, H2))
+        maxp = 4
+        sentinel = np.uint32(0xFFFFFFFF)
+        npk, used, status = (T(np.full(ids.size, sentinel, dtype=np.uint32).view(np.int32)) for _ in range(3))
+        pk = T(np.zeros(ids.size * maxp, dtype=np.int32))
+        frame = {"off": T(off.view(np.int64)), "len": T(L.view(np.int32)), "bound": 20480, "max_packets": maxp,
+                 "npk": npk, "used": used, "status": status, "pkt_len": pk}
+        pay = T(data)
+        c.crypt_grouped_declared(pay, T(off.view(np.int64)), T(L.view(np.int32)), T(ids.view(np.int32)),
+                                 groups, frame=frame, stream=s)
+        with pytest.raises(ZRC4Error) as ei:
+            c.sync(s)
+        assert ei.value.code == -7
+        got = pay.cpu().numpy()
+        bad = np.flatnonzero(got != want)
+        assert bad.size == 0, (bad[:8], int(bad.size))
+        g_npk, g_used, g_st = (t.cpu().numpy().view(np.uint32) for t in (npk, used, status))
+        refused = np.zeros(ids.size, dtype=bool)
+        refused[256 * 2: 256 * 3] = True
+        refused[256 * 5: 256 * 6] = True
+        if nb <= 256:
+            rb = refused & busy                           # the refused buckets' busy entries
+            assert rb.sum() == 51
+            assert (g_npk[rb] == sentinel).all() and (g_used[rb] == sentinel).all() \
+                and (g_st[rb] == sentinel).all(), "a refused bucket framed a busy entry over raw bytes"
+        w_npk, w_used, w_st, _ = pyoracle.frame_scan(want, off, L, 20480, maxp)
+        keep = ~refused
+        for name, w, g in (("npk", w_npk, g_npk), ("used", w_used, g_used), ("status", w_st, g_st)):
+            diff = np.flatnonzero(keep & (w != g))
+            assert diff.size == 0, (name, diff[:8].tolist(), w[diff[:4]].tolist(), g[diff[:4]].tolist())
+        _check_states(c, ob, cap)
