@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-6 randomised soak on the validated library (test-side only): the
+# 84-call C-ABI sweep (tests/test_gpu_fuzz.py) and the fused decrypt+frame
+# case (tests/test_frame_scan.py) from many seeds, one pytest process each.
+# ZRC4_SOAK_SEEDS='a-b' or 'a,b,c' (default 1-30); FUSED_SEEDS / FUZZ_SEEDS
+# override it per sweep, SOAK_SECS bounds each step (default 540).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=${SOAK_OUT:-gpurun_out/r06/soak}
+mkdir -p $OUT
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+export ZRC4_SOAK_SEEDS=${ZRC4_SOAK_SEEDS:-1-30}
+step() {  # name, seconds, command...
+    local name=$1 secs=$2; shift 2
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "[$name] rc=$rc"; grep -v amdgpu.ids "$OUT/$name.log" | tail -3 | cut -c1-600
+    if [ $rc -ne 0 ]; then echo "[$name] failed: stopping GPU work in this call"; exit $rc; fi
+}
+S=${SOAK_SECS:-540}
+ZRC4_SOAK_SEEDS=${FUSED_SEEDS:-$ZRC4_SOAK_SEEDS} step fused_soak $S python -u -m pytest tests/test_frame_scan.py -m gpu -k soak -x -v --durations=0 \
+    --timeout 240 --timeout-method thread -p no:cacheprovider
+ZRC4_SOAK_SEEDS=${FUZZ_SEEDS:-$ZRC4_SOAK_SEEDS} step fuzz_soak $S python -u -m pytest tests/test_gpu_fuzz.py -m gpu -k soak -x -v --durations=0 \
+    --timeout 240 --timeout-method thread -p no:cacheprovider
+echo soak done

@@ -13,6 +13,19 @@ sys.path.insert(0, str(ROOT / "oracle"))
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 
+def soak_seeds(default=(1,)):
+    """Seeds of the randomised GPU sweeps' soak cases: $ZRC4_SOAK_SEEDS as
+    'a-b' and/or 'a,b,c' (scripts/r06_soak.sh), else `default`."""
+    spec = os.environ.get("ZRC4_SOAK_SEEDS", "").strip()
+    if not spec:
+        return list(default)
+    out = []
+    for part in spec.split(","):
+        a, _, b = part.strip().partition("-")
+        out.extend(range(int(a), int(b) + 1) if b else [int(a)])
+    return out
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) device")
 

@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import pyoracle
+from conftest import soak_seeds
 
 BOUND = 20480
 
@@ -232,11 +233,34 @@ def test_fused_decrypt_and_frame(built, n, avg, mode):
     (half- and whole-group), ~587 behind the declared check on the
     persistent kernel.  Plaintext and framing
     against the oracle."""
+    _run_fused(n, avg, mode, seed=n + avg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", soak_seeds())
+def test_fused_decrypt_and_frame_soak(built, seed):
+    """A random fused decrypt+frame case per seed (one by default;
+    scripts/r06_soak.sh runs many through $ZRC4_SOAK_SEEDS): entry point,
+    session count on either side of every launch_crypt boundary (window,
+    half-group, whole-group, persistent with one to several chunks per
+    workgroup, ragged last groups), packet size, and how much of each block
+    an earlier iteration already decrypted."""
+    rng = np.random.default_rng(7000 + seed)
+    mode = ["range", "grouped", "declared"][int(rng.integers(0, 3))]
+    cls = int(rng.integers(0, 4))
+    n = int(rng.integers(*[(1, 8193), (8193, 32769), (32769, 65537), (65537, 300001)][cls]))
+    avg = int(rng.choice([40, 200, 900, 3000]))
+    avg = min(avg, max(40, 24_000_000 // n))              # <= ~48 MB of packets
+    tail = float(rng.choice([0.0, 0.5, 1.0]))
+    _run_fused(n, avg, mode, seed=seed, tail_frac=tail)
+
+
+def _run_fused(n, avg, mode, seed, tail_frac=0.5):
     import torch
     from zsummerx_amd import Context
     from zsummerx_amd._capi import IDLE_SLOT
     maxp = 8
-    buf, inp, off, ln, toff, tlen, keys = _fused_case(n, avg, seed=n + avg)
+    buf, inp, off, ln, toff, tlen, keys = _fused_case(n, avg, seed=seed, tail_frac=tail_frac)
     want = pyoracle.frame_scan(buf, off, ln, BOUND, maxp)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
     npk, used, status = (torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3))

@@ -20,6 +20,7 @@ import numpy as np
 import pytest
 
 import pyoracle
+from conftest import soak_seeds
 from zsummerx_amd import Context
 from zsummerx_amd._capi import IDLE_SLOT
 
@@ -44,9 +45,20 @@ def _layout(rng, n, scale):
 
 
 def test_random_call_sequence(built):
+    _run_sequence(20260518)
+
+
+@pytest.mark.parametrize("seed", soak_seeds())
+def test_random_call_sequence_soak(built, seed):
+    """The same sweep from other seeds (one by default; scripts/r06_soak.sh
+    runs many in one process through $ZRC4_SOAK_SEEDS)."""
+    _run_sequence(1000 + seed)
+
+
+def _run_sequence(seed):
     import torch
     assert torch.cuda.is_available(), "gpu tests need a GPU"
-    rng = np.random.default_rng(20260518)
+    rng = np.random.default_rng(seed)
     cap = 256 * GROUPS
     keys = rng.integers(0, 256, 16 * cap, dtype=np.uint8)
     koff = np.arange(cap, dtype=np.uint64) * 16
