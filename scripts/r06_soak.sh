@@ -1,9 +1,11 @@
 #!/bin/bash
 # Round-6 randomised soak on the validated library (test-side only): the
 # 84-call C-ABI sweep (tests/test_gpu_fuzz.py) and the fused decrypt+frame
-# case (tests/test_frame_scan.py) from many seeds, one pytest process each.
+# case (tests/test_frame_scan.py) from many seeds, one pytest process each;
+# ENGINE_SEEDS adds the engine's echo parity (tests/test_frame.py) on the
+# device hooks.
 # ZRC4_SOAK_SEEDS='a-b' or 'a,b,c' (default 1-30); FUSED_SEEDS / FUZZ_SEEDS
-# override it per sweep, SOAK_SECS bounds each step (default 540).
+# override it per sweep ('none' skips one), SOAK_SECS bounds each step (default 540).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${SOAK_OUT:-gpurun_out/r06/soak}
@@ -18,8 +20,12 @@ step() {  # name, seconds, command...
     if [ $rc -ne 0 ]; then echo "[$name] failed: stopping GPU work in this call"; exit $rc; fi
 }
 S=${SOAK_SECS:-540}
-ZRC4_SOAK_SEEDS=${FUSED_SEEDS:-$ZRC4_SOAK_SEEDS} step fused_soak $S python -u -m pytest tests/test_frame_scan.py -m gpu -k soak -x -v --durations=0 \
+[ "${FUSED_SEEDS:-}" != none ] && ZRC4_SOAK_SEEDS=${FUSED_SEEDS:-$ZRC4_SOAK_SEEDS} step fused_soak $S python -u -m pytest tests/test_frame_scan.py -m gpu -k soak -x -v --durations=0 \
     --timeout 240 --timeout-method thread -p no:cacheprovider
-ZRC4_SOAK_SEEDS=${FUZZ_SEEDS:-$ZRC4_SOAK_SEEDS} step fuzz_soak $S python -u -m pytest tests/test_gpu_fuzz.py -m gpu -k soak -x -v --durations=0 \
+[ "${FUZZ_SEEDS:-}" != none ] && ZRC4_SOAK_SEEDS=${FUZZ_SEEDS:-$ZRC4_SOAK_SEEDS} step fuzz_soak $S python -u -m pytest tests/test_gpu_fuzz.py -m gpu -k soak -x -v --durations=0 \
     --timeout 240 --timeout-method thread -p no:cacheprovider
+if [ -n "${ENGINE_SEEDS:-}" ]; then
+ZRC4_SOAK_SEEDS=$ENGINE_SEEDS step engine_soak $S python -u -m pytest tests/test_frame.py -m gpu -k soak -x -v \
+    --durations=0 --timeout 240 --timeout-method thread -p no:cacheprovider
+fi
 echo soak done

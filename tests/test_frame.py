@@ -21,7 +21,7 @@ import threading
 
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, soak_seeds
 
 STRESS = __import__('pathlib').Path(__import__('os').environ.get('ZSX_STRESS', str(ROOT / 'zsummerx_amd' / 'bin' / 'frame_stress')))
 ORACLE_HOOKS = "host:" + str(ROOT / "oracle" / "liboracle.so")
@@ -125,10 +125,10 @@ def echo_client(port, seed, npk, results, idx, keyed=True):
     results[idx] = (plain, bytes(got), rd.encryption(bytes(got)))
 
 
-def run_echo_parity(stress, hooks, nclients=6, npk=40, extra=()):
+def run_echo_parity(stress, hooks, nclients=6, npk=40, extra=(), seed0=1000):
     srv = Server(stress, hooks, nclients, *extra)
     results = [None] * nclients
-    th = [threading.Thread(target=echo_client, args=(srv.port, 1000 + i, npk, results, i)) for i in range(nclients)]
+    th = [threading.Thread(target=echo_client, args=(srv.port, seed0 + i, npk, results, i)) for i in range(nclients)]
     for t in th:
         t.start()
     for t in th:
@@ -347,6 +347,19 @@ def test_no_device_is_loud(stress):
 def test_engine_echo_parity_device(stress):
     st = run_echo_parity(stress, "device")
     assert st["rc4"] == "zrc4-gfx950"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", soak_seeds())
+def test_engine_echo_parity_device_soak(stress, seed):
+    """Echo parity from other seeds (one by default; scripts/r06_soak.sh runs
+    many through $ZRC4_SOAK_SEEDS): reservoir, direct or direct with device
+    framing, 2-16 clients, 10-60 packets each, random chunkings."""
+    rng = random.Random(9000 + seed)
+    hooks, extra = rng.choice([("device", ()), ("device-direct", ()), ("device-direct", ("--device-framing",))])
+    st = run_echo_parity(stress, hooks, nclients=rng.randint(2, 16), npk=rng.randint(10, 60), extra=extra,
+                         seed0=100_000 * seed)
+    assert st["rc4"].startswith("zrc4-gfx950")
 
 
 @pytest.mark.gpu
