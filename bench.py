@@ -882,6 +882,9 @@ def parse(argv=None):
                    help="with --host-inclusive: chunks of the batch (0 = by size, host_chunks: one up to 32 MiB, "
                         "else one per 32 MiB, at most 16; tools/hostinc_sweep.py)")
     p.add_argument("--streams", type=int, default=4)
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="N > 1 on a one-GPU box: every rank on cuda:0 over gloo (scripts/r06_rehearse.sh); "
+                        "exercises the multi-rank path end to end, its times are no scaling measurement")
     return p.parse_args(argv)
 
 
@@ -1030,6 +1033,8 @@ def rank_main(args, backend="nccl", make_runner=None):
     """One rank of the bench (torchrun's, self_launch's or the only one)."""
     import torch.distributed as dist
     ws, rank, local = dist_env()
+    if getattr(args, "rehearse_one_gpu", False):
+        backend, local = "gloo", 0
     if ws != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE")
     res, runner = run_bench(args, ws, rank, local, backend, make_runner, own_pg=False)
@@ -1045,6 +1050,8 @@ def rank_main(args, backend="nccl", make_runner=None):
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
+        if getattr(args, "rehearse_one_gpu", False):
+            res["config"]["rehearsal"] = "gloo, every rank on cuda:0: the multi-rank path, not a scaling measurement"
         print(json.dumps(res), flush=True)
     return res
 

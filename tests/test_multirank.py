@@ -146,6 +146,29 @@ def test_self_launch_two_ranks(capsys):
     assert abs(comp["value"] - expect) <= 0.02 * expect + 2e-3
 
 
+@pytest.mark.timeout(300)
+def test_self_launch_rehearsal_puts_every_rank_on_device_0(capsys, monkeypatch):
+    """`--rehearse-one-gpu` (scripts/r06_rehearse.sh: the multi-rank path on a
+    one-GPU box): every rank takes device 0 whatever LOCAL_RANK says, the
+    group is gloo, and the line says it is a rehearsal."""
+    import bench
+    argv = ["--gpus", "2", "--workload", "tiny", "--steps", "2", "--warmup", "1", "--footprint-mib", "0",
+            "--cpu-seconds", "0", "--companion-workload", "none", "--rehearse-one-gpu"]
+    rc = bench.self_launch(argv, 2, entry=ROOT / "tests" / "bench_child_cpu.py", timeout=240)
+    out = capsys.readouterr().out
+    assert rc == 0, out
+    res = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+    assert res["n_gpus"] == 2 and res["config"]["dist_backend"] == "gloo"
+    assert "rehearsal" in res["config"]
+    seen = []
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    monkeypatch.setattr(bench, "run_bench", lambda a, ws, rank, local, backend, *r, **k: (
+        seen.append((local, backend)), ({"config": {}}, None))[1])
+    bench.rank_main(bench.parse(["--rehearse-one-gpu", "--companion-workload", "none"]))
+    assert seen == [(0, "gloo")]
+
+
 @pytest.mark.timeout(120)
 def test_self_launch_reports_a_failing_rank(capsys):
     """A rank that fails makes the job fail (non-zero exit), and the other
