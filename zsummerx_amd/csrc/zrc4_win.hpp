@@ -88,6 +88,18 @@ struct WinLane {
 #ifndef ZRC4_WIN_SDWA
 #define ZRC4_WIN_SDWA 0
 #endif
+// ZRC4_WIN_ALIGN (A/B only): the loop head aligned to 2^N bytes (s_nop padding
+// before it, run once); 0 = no directive (the default ISA).
+#ifndef ZRC4_WIN_ALIGN
+#define ZRC4_WIN_ALIGN 0
+#endif
+#define ZW_STR2(x) #x
+#define ZW_STR(x) ZW_STR2(x)
+#if ZRC4_WIN_ALIGN
+#define ZW_LOOP_ALIGN ".p2align " ZW_STR(ZRC4_WIN_ALIGN) "\n\t"
+#else
+#define ZW_LOOP_ALIGN ""
+#endif
 #define ZW_ADDR(XA)                                                                               \
     "v_add_u32_sdwa v106, " XA ", %[l] dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "  \
     "src1_sel:DWORD\n\t"
@@ -104,6 +116,7 @@ __device__ __forceinline__ void win_windows(WinLane &w, uint32_t rem, uint32_t l
         "v_mov_b32 v126, %[sb]\n\t"
         ZW_ADDR("%[xa]")
         "ds_read_u8 v107, v106\n\t"                             // a_l of window 0
+        ZW_LOOP_ALIGN
         "ZW_LOOP_%=:\n\t"
         // 1. scan of a, tail of window n-1
         "s_waitcnt lgkmcnt(0)\n\t"
