@@ -564,7 +564,10 @@ int zrc4_ksa_host(zrc4_ctx *c, const uint32_t *ids, const uint8_t *keys, size_t 
     }
     rc = launch_ksa(c, ids ? (const uint32_t *)(st + o_ids) : nullptr, 0,
                     st + o_key, (const uint64_t *)(st + o_off), (const uint32_t *)(st + o_len), n, c->stream);
-    if (rc) return rc;
+    if (rc) {
+        (void)hipStreamSynchronize(c->stream);     // a queued H2D still reads the staging buffer
+        return rc;
+    }
     return check_err(c, c->stream);
 }
 
@@ -752,13 +755,19 @@ int zrc4_crypt_host(zrc4_ctx *c, const uint32_t *ids, uint8_t *payload, size_t p
                       (const uint32_t *)(st + o_len), m, c->stream, nullptr, grouped ? bgroup.data() : nullptr,
                       true);
     if (rc) {
-        if (piped) (void)hipStreamSynchronize(c->stream);
+        // whatever was queued before the failure (the H2D copies, a check
+        // kernel reading the zero-copy tables) still reads the staging
+        // buffer, which the next call rewrites: drain it first
+        (void)hipStreamSynchronize(c->stream);
         return rc;
     }
     if (piped) return copy_back_piped(c, payload, o_pay, payload_bytes);
-    if (payload_bytes && !zero_copy)
-        ZRC4_TRY(hipMemcpyAsync(c->h_stage + o_pay, c->d_stage + o_pay, payload_bytes,
-                                hipMemcpyDeviceToHost, c->stream));
+    if (payload_bytes && !zero_copy &&
+        hipMemcpyAsync(c->h_stage + o_pay, c->d_stage + o_pay, payload_bytes, hipMemcpyDeviceToHost,
+                       c->stream) != hipSuccess) {
+        (void)hipStreamSynchronize(c->stream);
+        return ZRC4_ERR_HIP;
+    }
     rc = check_err(c, c->stream);
     if (rc) return rc;
     if (payload_bytes) par_memcpy(payload, c->h_stage + o_pay, payload_bytes);
