@@ -503,6 +503,53 @@ __device__ __forceinline__ uint32_t head_bytes(const uint8_t *msg, uint32_t len)
     "s_waitcnt vmcnt(8)\n\t"                                                                     \
     ZL_BLOCK(v56, v57, v58, v59, v60, v61, v62, v63, v64, v65, v66, v67, v68, v69, v70, v71)    \
     ZL_STORE(ZL_B0, ZL_B1, ZL_B2, ZL_B3)
+// ZRC4_BLK_DEFER (A/B, default 0 = the ISA above): each block's keystream
+// goes into K first (byte moves, as block 0's does) and the wait for the
+// block's payload comes after it, so a block's loads have two blocks of
+// keystream time to land instead of one (+16 VALU per block for the XOR).
+#ifndef ZRC4_BLK_DEFER
+#define ZRC4_BLK_DEFER 0
+#endif
+#define ZL_MOVK(R, SEL, K)                                                                       \
+    "v_mov_b32_sdwa " #R ", %[" #K "] dst_sel:" #SEL " dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0\n\t"
+#define ZL_W0K(D)                                                                                \
+    ZRC4_E ZRC4_O ZL_MOVK(D, BYTE_0, k0) ZRC4_E ZL_MOVK(D, BYTE_1, k1)                          \
+    ZRC4_O ZL_MOVK(D, BYTE_2, k0)
+#define ZL_WK(DP, D)                                                                             \
+    ZRC4_E ZL_MOVK(DP, BYTE_3, k1) ZRC4_O ZL_MOVK(D, BYTE_0, k0)                                \
+    ZRC4_E ZL_MOVK(D, BYTE_1, k1) ZRC4_O ZL_MOVK(D, BYTE_2, k0)
+#define ZL_BLOCKK                                                                                \
+    ZL_W0K(v72) ZL_WK(v72, v73) ZL_WK(v73, v74) ZL_WK(v74, v75) ZL_WK(v75, v76) ZL_WK(v76, v77)   \
+    ZL_WK(v77, v78) ZL_WK(v78, v79) ZL_WK(v79, v80) ZL_WK(v80, v81) ZL_WK(v81, v82)               \
+    ZL_WK(v82, v83) ZL_WK(v83, v84) ZL_WK(v84, v85) ZL_WK(v85, v86) ZL_WK(v86, v87)               \
+    "s_waitcnt lgkmcnt(0)\n\t" ZL_MOVK(v87, BYTE_3, k1)
+#define ZL_KXOR(d0, d1, d2, d3, d4, d5, d6, d7, d8, d9, d10, d11, d12, d13, d14, d15)            \
+    "v_xor_b32_e32 " #d0 ", " #d0 ", v72\n\tv_xor_b32_e32 " #d1 ", " #d1 ", v73\n\t"                 \
+    "v_xor_b32_e32 " #d2 ", " #d2 ", v74\n\tv_xor_b32_e32 " #d3 ", " #d3 ", v75\n\t"                 \
+    "v_xor_b32_e32 " #d4 ", " #d4 ", v76\n\tv_xor_b32_e32 " #d5 ", " #d5 ", v77\n\t"                 \
+    "v_xor_b32_e32 " #d6 ", " #d6 ", v78\n\tv_xor_b32_e32 " #d7 ", " #d7 ", v79\n\t"                 \
+    "v_xor_b32_e32 " #d8 ", " #d8 ", v80\n\tv_xor_b32_e32 " #d9 ", " #d9 ", v81\n\t"                 \
+    "v_xor_b32_e32 " #d10 ", " #d10 ", v82\n\tv_xor_b32_e32 " #d11 ", " #d11 ", v83\n\t"             \
+    "v_xor_b32_e32 " #d12 ", " #d12 ", v84\n\tv_xor_b32_e32 " #d13 ", " #d13 ", v85\n\t"             \
+    "v_xor_b32_e32 " #d14 ", " #d14 ", v86\n\tv_xor_b32_e32 " #d15 ", " #d15 ", v87\n\t"
+#if ZRC4_BLK_DEFER
+#undef ZL_HALF_A
+#undef ZL_HALF_B
+#define ZL_HALF_A                                                                                \
+    ZL_ACTIVE                                                                                    \
+    ZL_PREFETCH(ZL_B0, ZL_B1, ZL_B2, ZL_B3)                                                      \
+    ZL_BLOCKK                                                                                    \
+    "s_waitcnt vmcnt(8)\n\t"                                                                     \
+    ZL_KXOR(v40, v41, v42, v43, v44, v45, v46, v47, v48, v49, v50, v51, v52, v53, v54, v55)     \
+    ZL_STORE(ZL_A0, ZL_A1, ZL_A2, ZL_A3)
+#define ZL_HALF_B                                                                                \
+    ZL_ACTIVE                                                                                    \
+    ZL_PREFETCH(ZL_A0, ZL_A1, ZL_A2, ZL_A3)                                                      \
+    ZL_BLOCKK                                                                                    \
+    "s_waitcnt vmcnt(8)\n\t"                                                                     \
+    ZL_KXOR(v56, v57, v58, v59, v60, v61, v62, v63, v64, v65, v66, v67, v68, v69, v70, v71)     \
+    ZL_STORE(ZL_B0, ZL_B1, ZL_B2, ZL_B3)
+#endif
 #define ZL_FIRST                                                                                 \
     "s_mov_b32 %[i], 0\n\t"                                                                      \
     ZL_PREFETCH(ZL_B0, ZL_B1, ZL_B2, ZL_B3)                                                      \
