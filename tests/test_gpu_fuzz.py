@@ -138,3 +138,43 @@ def _run_sequence(seed):
     # the sweep reached the window and the persistent kernels with grouped ids
     assert any(m in ("grouped", "declared") and g <= 32 for m, g, _ in seen), seen
     assert any(m in ("grouped", "declared") and g > 256 for m, g, _ in seen), seen
+
+
+@pytest.mark.parametrize("seed", soak_seeds())
+def test_ksa_soak(built, seed):
+    """Batched makeSBox (rc4_encryption.h:46-72) from random seeds (one by
+    default; scripts/r06_soak.sh runs many through $ZRC4_SOAK_SEEDS): 1-6 000
+    keys whose lengths hit every ksa_kernel path half the time (0, the
+    register patterns 1-64, the LDS window's edges 48-50, the per-step fetch
+    up to 300) and are uniform in 0..300 otherwise, NUL-rich, at random
+    alignments, through zrc4_ksa_range at a random (often unaligned) first
+    slot or zrc4_ksa with random ids; every state against the oracle."""
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    rng = np.random.default_rng(5000 + seed)
+    n = int(rng.integers(1, 6001))
+    edges = np.array([0, 1, 2, 4, 8, 16, 31, 32, 33, 48, 49, 50, 63, 64, 65, 128, 255, 256, 257, 300])
+    klen = np.where(rng.random(n) < 0.5, rng.choice(edges, n), rng.integers(0, 301, n)).astype(np.uint32)
+    gaps = rng.integers(0, 17, n)
+    koff = np.cumsum(np.concatenate([[gaps[0]], klen[:-1].astype(np.int64) + gaps[1:]])).astype(np.uint64)
+    keys = rng.integers(0, 256, int(koff[-1] + klen[-1]) + 8, dtype=np.uint8)
+    keys[rng.random(keys.size) < 0.1] = 0
+    cap = 256 * (-(-n // 256) + 2)
+    ob = pyoracle.Batch(n)
+    ob.make_sbox(keys, koff, klen)
+    osb, ox, oy = ob.states()
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    s = torch.cuda.current_stream()
+    with Context(0, cap) as c:
+        if rng.random() < 0.5:
+            first = int(rng.integers(0, cap - n + 1))
+            slots = first + np.arange(n)
+            c.ksa_range(first, T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys), stream=s)
+        else:
+            slots = rng.permutation(cap)[:n]
+            c.ksa(T(klen.view(np.int32)), T(koff.view(np.int64)), T(keys),
+                  ids=T(slots.astype(np.uint32).view(np.int32)), stream=s)
+        c.sync(s)
+        gsb, gx, gy = c.get_states(0, cap)
+    bad = np.flatnonzero((gsb[slots] != osb).any(axis=1) | (gx[slots] != ox) | (gy[slots] != oy))
+    assert bad.size == 0, (n, bad[:8].tolist(), klen[bad[:8]].tolist(), int(bad.size))
