@@ -347,7 +347,11 @@ public:
             level_.resize(zrc4_capacity(ctx_));
             ringSlab_.assign(zrc4_capacity(ctx_) / ZRC4_GROUP_SLOTS, nullptr);
             hungryMark_.assign(zrc4_capacity(ctx_), 0u);
-            refillChunk_ = std::max<uint32_t>(256u, std::min<uint32_t>(kRefillChunk, ringCap_ / 4));
+            // $ZSX_REFILL_CHUNK (A/B knob): bytes per slot per refill, at most a
+            // quarter of the ring (two refills in flight leave half of it readable)
+            const char *rc = std::getenv("ZSX_REFILL_CHUNK");
+            const uint32_t want = rc ? (uint32_t)std::strtoul(rc, nullptr, 10) : kRefillChunk;
+            refillChunk_ = std::max<uint32_t>(256u, std::min<uint32_t>(want, ringCap_ / 4));
         }
     }
     ~DeviceRc4Hooks() override { release(); }
@@ -764,7 +768,11 @@ private:
         ctx_ = nullptr;
     }
 
-    static constexpr uint32_t kRefillChunk = 8192;
+    // 16 KiB per slot per refill (r06; 8 KiB before): a refill launch pays
+    // ~6 us of launch, state load and store around its serial chain, and a
+    // few-session engine is bound by that chain (config 1: 113.3k -> 117.0k
+    // echo/s, scripts/r06_refill_ab.sh)
+    static constexpr uint32_t kRefillChunk = 16384;
     static constexpr uint32_t kRefillDepth = 2;
     const uint32_t refillDepth_ = std::getenv("ZSX_REFILL_DEPTH") ? std::max(1, std::min(2, std::atoi(std::getenv("ZSX_REFILL_DEPTH")))) : kRefillDepth;
     static constexpr int ZRC4_ERR_NOT_READY_ = 1;   // internal: oldest refill still running
